@@ -1,0 +1,222 @@
+/*
+ * mmfd.h — C ABI of libmmfd_hip.so, the MI355X (gfx950) kernels behind the multimodal
+ * misinformation-detection training hot path.
+ *
+ * The reference (sakdag/multimodal-misinformation-detection) is pure Python: its "interface" for
+ * this path is a set of torch.nn modules and torch ops. Each entry point below names the
+ * reference call sites it replaces (file:line, relative to the reference repo root).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer unless documented otherwise; the library never allocates,
+ *     frees or synchronises; work is enqueued on `stream` (a hipStream_t; NULL = default stream);
+ *   - tensors are dense row-major with an explicit leading dimension (elements, not bytes);
+ *   - `dtype` is MMFD_F32 or MMFD_BF16 (storage type of activations / operands); accumulation,
+ *     LayerNorm statistics, softmax statistics, optimizer state and all gradients of parameters are
+ *     fp32;
+ *   - return value 0 = success; otherwise an MMFD_ERR_* or hipError_t code, and
+ *     mmfd_last_error_string() describes it (thread-local).
+ *   - dropout is counter based: element e of call-site `salt` is dropped iff
+ *     hash(*seed, salt, e) < p * 2^32 (hash = mmfd_hash in csrc/common.h), so backward kernels
+ *     regenerate the forward mask and a CPU oracle can reproduce it exactly.
+ */
+#ifndef MMFD_H_
+#define MMFD_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mmfd_stream_t; /* hipStream_t */
+
+enum { MMFD_F32 = 0, MMFD_BF16 = 1 };
+enum {
+  MMFD_ACT_NONE = 0,
+  MMFD_ACT_GELU = 1,      /* exact erf GELU, nn.GELU() (layers.py:14) / HF "gelu" */
+  MMFD_ACT_RELU = 2,      /* nn.ReLU() (model.py:264 ...) */
+  MMFD_ACT_GELU_BWD = 3,  /* out *= gelu'(aux)  (aux = saved pre-activation) */
+  MMFD_ACT_RELU_BWD = 4   /* out *= (aux > 0)   */
+};
+enum { MMFD_OK = 0, MMFD_ERR_INVALID = 1000, MMFD_ERR_UNSUPPORTED = 1001 };
+
+/* ------------------------------------------------------------------------------------------- */
+/* library                                                                                      */
+/* ------------------------------------------------------------------------------------------- */
+const char* mmfd_last_error_string(void);
+int mmfd_version(void);
+/* 32-bit dropout hash (host copy of the device function), for tests and the CPU oracle. */
+uint32_t mmfd_dropout_hash(uint64_t seed, uint64_t salt, uint64_t index);
+
+/* ------------------------------------------------------------------------------------------- */
+/* GEMM with fused epilogue.                                                                    */
+/* Replaces every nn.Linear forward/backward on the path: src/model/model.py:19-36, 137-152,   */
+/* 252-288, 395-403; src/model/layers.py:12-18, 57 (out_proj); the HF BERT/ViT projections      */
+/* called at train.py:137-143; the ViT patch conv (GEMM over patches).                         */
+/*   C[m][n] = epilogue( alpha * sum_k A(m,k) B(k,n) ) (+ beta * C_old[m][n])                  */
+/*   A(m,k) = trans_a ? A[k*lda + m] : A[m*lda + k]                                             */
+/*   B(k,n) = trans_b ? B[k*ldb + n] : B[n*ldb + k]     (trans_b=0 is nn.Linear's W[N][K])     */
+/* Epilogue order: z = alpha*acc + bias[n]; if act is a forward act: aux <- z, z = act(z);      */
+/*   if act is a backward act: z *= act'(aux); dropout(z); z += residual; z += beta*C_old.      */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct mmfd_epilogue {
+  const float* bias;       /* [N] fp32, or NULL */
+  const void* residual;    /* [M][ldr] in c_dtype, or NULL */
+  int64_t ldr;
+  void* aux;               /* [M][ldaux] in c_dtype: written by GELU/RELU, read by *_BWD */
+  int64_t ldaux;
+  int act;                 /* MMFD_ACT_* */
+  float dropout_p;         /* 0 disables */
+  const uint64_t* seed;    /* device pointer to the step seed (read by the kernel) */
+  uint64_t salt;           /* call-site id; element index = m * N + n */
+} mmfd_epilogue;
+
+typedef struct mmfd_gemm_args {
+  int dtype;               /* operand dtype of A and B */
+  int trans_a, trans_b;
+  int64_t M, N, K;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc; int c_dtype;
+  float alpha, beta;
+  mmfd_epilogue ep;
+  void* workspace; int64_t workspace_bytes; /* split-K fp32 slabs; may be NULL (no split) */
+  int splits;              /* 0 = choose automatically (bounded by workspace_bytes) */
+} mmfd_gemm_args;
+
+int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);
+/* bytes of workspace the automatic split choice would like for this problem */
+int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* args);
+
+/* Column sums (bias gradients): out[n] = beta*out[n] + sum_m X[m*ldx + n]. workspace >= 4*N*256 B */
+int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, float* out, float beta,
+                void* workspace, int64_t workspace_bytes, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* Multi-head attention (unmasked fusion-head MHA layers.py:36-58 incl. the SDPA branch 44-49;  */
+/* HF BERT/ViT/MPNet self-attention called at train.py:137-143).                              */
+/* Q/K/V/O are addressed per (batch b, token t, head h) as base + b*s_b + t*s_t + h*D.         */
+/*   S = scale * Q K^T (+ key_bias[b][k]) (+ rel_bias[h][q][k]);  P = softmax(S);              */
+/*   O = dropout(P) V ;   lse[b][h][q] = log sum_k exp(S) (fp32)                                */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct mmfd_attn_args {
+  int dtype;
+  int64_t B, H, Lq, Lk, D;         /* D in {32, 64} */
+  float scale;
+  const void* q; int64_t q_sb, q_st;
+  const void* k; int64_t k_sb, k_st;
+  const void* v; int64_t v_sb, v_st;
+  void* o; int64_t o_sb, o_st;
+  float* lse;                      /* [B][H][Lq] */
+  const float* key_bias;           /* [B][Lk] additive (HF extended attention mask) or NULL */
+  const float* rel_bias;           /* [H][Lq][Lk] additive (MPNet relative position) or NULL */
+  float dropout_p; const uint64_t* seed; uint64_t salt;  /* index = ((b*H+h)*Lq+q)*Lk+k */
+  /* backward only */
+  const void* dout; int64_t do_sb, do_st;   /* same head layout as o */
+  void* dq; int64_t dq_sb, dq_st;
+  void* dk; int64_t dk_sb, dk_st;
+  void* dv; int64_t dv_sb, dv_st;
+  float* delta;                    /* workspace [B][H][Lq] fp32 */
+  float* d_rel_bias;               /* must be NULL (the relative bias is inference-only, MPNet) */
+  int accumulate_dq;               /* 1: dq += result (else overwrite) */
+  int accumulate_dkv;              /* 1: dk += ..., dv += ... */
+} mmfd_attn_args;
+
+int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);
+int mmfd_attn_bwd(const mmfd_attn_args* args, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* LayerNorm over the last dim (fusion head nn.LayerNorm model.py:39-46, 155-162, eps 1e-5;     */
+/* BERT/ViT LayerNorm eps 1e-12). mean/rstd are saved per row (fp32).                          */
+/* ------------------------------------------------------------------------------------------- */
+int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
+                       const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
+                       float* mean, float* rstd, mmfd_stream_t stream);
+/* dx = LN'(dy) (+ dx_add); dgamma/dbeta (fp32, [width]) are written (beta_acc=0) or accumulated
+ * (beta_acc=1) through a deterministic two-pass reduction; workspace >= 8*width*256 bytes.
+ * If dx_drop != NULL it also receives dropout(dx) for call-site (seed, salt, p) with element
+ * index row*width+col (the mask the producing GEMM epilogue applied). */
+int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
+                       const void* x, int64_t ldx, const float* gamma, const float* mean,
+                       const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
+                       float* dgamma, float* dbeta, float beta_acc, void* dx_drop,
+                       float dropout_p, const uint64_t* seed, uint64_t salt,
+                       void* workspace, int64_t workspace_bytes, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* Sequence mean pooling S.mean(dim=1) (model.py:308-317, 332-345, 448)                         */
+/* ------------------------------------------------------------------------------------------- */
+int mmfd_seq_mean_fwd(int dtype, int64_t B, int64_t L, int64_t D, const void* x, void* out,
+                      int64_t ldo, mmfd_stream_t stream);
+int mmfd_seq_mean_bwd(int dtype, int64_t B, int64_t L, int64_t D, const void* dout, int64_t ldo,
+                      void* dx, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* Summed per-path cross entropy (train.py:165-169: sum_i CrossEntropyLoss(y_i, labels[:, i])).  */
+/* logits: n_paths pointers (device array of device pointers) each [B][C] fp32; labels int64    */
+/* [B][label_ld] with path i in column i. loss[0] = total, loss[1+i] = path i (mean over B).     */
+/* dlogits (optional, n_paths pointers) receive d(total)/d(logits) * (*dloss_scale or 1).        */
+/* ------------------------------------------------------------------------------------------- */
+int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits,
+                      const int64_t* labels, int64_t label_ld, float* loss, float* const* dlogits,
+                      const float* dloss_scale, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* BERT embeddings (HF BertEmbeddings: word + position + token_type, LayerNorm, dropout).       */
+/* ------------------------------------------------------------------------------------------- */
+int mmfd_embed_ln_fwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                      const int64_t* token_type_ids, const float* word, const float* pos,
+                      const float* type, const float* gamma, const float* beta, float eps,
+                      void* sum_out, void* y, float* mean, float* rstd, float dropout_p,
+                      const uint64_t* seed, uint64_t salt, mmfd_stream_t stream);
+/* scatter-add the gradient of the pre-LN sum into the three tables (fp32 atomics for word). */
+int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                   const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos,
+                   float* dtype_emb, int64_t padding_idx, mmfd_stream_t stream);
+/* key-padding mask (int64 0/1) -> additive bias (0 or `neg`, HF uses finfo(float32).min) */
+int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, float neg, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* ViT patch embedding support (HF ViTPatchEmbeddings conv16/s16 == GEMM over patches).         */
+/* patchify: pixels fp32 [B][C][Hh][Ww] -> out [B*np][C*P*P] in dtype (c, kh, kw order).        */
+/* tokens: out[b][0] = cls + pos[0]; out[b][1+p] = patch[b*np+p] + pos[1+p].                     */
+/* ------------------------------------------------------------------------------------------- */
+int mmfd_patchify(int dtype, int64_t B, int64_t C, int64_t Hh, int64_t Ww, int64_t P,
+                  const float* pixels, void* out, mmfd_stream_t stream);
+int mmfd_vit_tokens_fwd(int dtype, int64_t B, int64_t NP, int64_t D, const void* patch,
+                        const float* cls, const float* pos, void* out, mmfd_stream_t stream);
+int mmfd_vit_tokens_bwd(int dtype, int64_t B, int64_t NP, int64_t D, const void* dout, void* dpatch,
+                        float* dcls, float* dpos, void* workspace, int64_t workspace_bytes,
+                        mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* AdamW (torch.optim.AdamW defaults as used at train.py:356/188), multi-tensor, one launch.    */
+/* table: device array of n_tensors records {param f32*, grad f32*, exp_avg f32*, exp_avg_sq     */
+/* f32*, param_bf16 bf16* (optional shadow copy, may be NULL), step f32*, numel};             */
+/* max_numel = largest numel. Step counters live in device memory: the launch first increments */
+/* every *step, then updates with the new values, so a captured hipGraph replays correctly.     */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct mmfd_adamw_tensor {
+  float* param; const float* grad; float* exp_avg; float* exp_avg_sq; void* param_bf16;
+  float* step;             /* per-tensor step counter (device fp32, like torch's state['step']) */
+  int64_t numel;
+} mmfd_adamw_tensor;
+int mmfd_adamw(int n_tensors, const mmfd_adamw_tensor* table, int64_t max_numel, float lr,
+               float beta1, float beta2, float eps, float weight_decay, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* elementwise helpers                                                                          */
+/* ------------------------------------------------------------------------------------------- */
+/* out(dtype_out) = in(dtype_in) * scale (+ add) — casts / scaled copies / grad accumulation. */
+int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream);
+int mmfd_axpby(int dtype, int64_t n, float a, const void* x, float b, const void* y, void* out,
+               mmfd_stream_t stream);
+/* generic dropout (out = keep ? x/(1-p) : 0), index = element index. */
+int mmfd_dropout(int dtype, int64_t n, const void* x, void* out, float p, const uint64_t* seed,
+                 uint64_t salt, mmfd_stream_t stream);
+/* seed[0] += 1 (advances the step seed inside a captured graph) */
+int mmfd_seed_advance(uint64_t* seed, mmfd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMFD_H_ */

@@ -1,0 +1,554 @@
+// Flash-style multi-head attention for gfx950 (head_dim 32 or 64, L <= a few hundred).
+//
+// Replaces: src/model/layers.py:36-58 (MultiHeadAttention, eager and SDPA branches; no mask) and the
+// self-attention of the HF BERT / ViT / MPNet encoders called at train.py:137-143 (key padding mask
+// as an additive per-key bias, MPNet relative-position bias as an additive [H][Lq][Lk] bias).
+//
+// Every product runs on 16x16 MFMAs (bf16: 16x16x32, fp32: 16x16x4). Work split:
+//   forward  : workgroup = (b, h, 64 queries), wave = 16 queries; loops over 64-key blocks staged
+//              in LDS. S^T = K Q^T puts the query on the lane, so the online-softmax statistics are
+//              lane-local (reduced over 4 lanes) and P^T's accumulator is directly the A operand of
+//              O = P V (keys in the "split" order {4g..4g+3, 16+4g..16+4g+3}); V is read with the
+//              hardware-transposing ds_read_b64_tr_b16.
+//   backward : two kernels, no atomics (deterministic): dK/dV per 64-key block looping over query
+//              blocks (S = Q K^T puts the key on the lane: P and dS are directly the A operands of
+//              dV = P^T dO and dK = dS^T Q), and dQ per 64-query block looping over key blocks
+//              (S^T again). delta = rowsum(dO * O) comes from a small kernel first.
+// Dropout on P (layers.py:53 / SDPA dropout_p) is counter based: index ((b*H+h)*Lq+q)*Lk+k.
+#include "common.h"
+#include <algorithm>
+#include <math.h>
+
+namespace {
+
+struct AttnP {
+  int64_t B, H, Lq, Lk;
+  float scale;
+  const void* q; int64_t q_sb, q_st;
+  const void* k; int64_t k_sb, k_st;
+  const void* v; int64_t v_sb, v_st;
+  void* o; int64_t o_sb, o_st;
+  float* lse;
+  const float* key_bias;
+  const float* rel_bias;
+  float p; uint32_t thr; float keep_scale;
+  const uint64_t* seed; uint64_t salt;
+  const void* dout; int64_t do_sb, do_st;
+  void* dq; int64_t dq_sb, dq_st;
+  void* dk; int64_t dk_sb, dk_st;
+  void* dv; int64_t dv_sb, dv_st;
+  float* delta;
+  int acc_dq, acc_dkv;
+};
+
+template <typename T, int D>
+struct AT {
+  static constexpr int ESZ = sizeof(T);
+  static constexpr int RB = D * ESZ;          // bytes per row
+  static constexpr int NCH = RB / 16;         // 16-B chunks per row
+  static constexpr int EPC = 16 / ESZ;
+  static constexpr int KCH = D / Mma<T>::KC;  // MFMA chunks along D
+  static constexpr int TILE = 64 * RB;        // one 64-row image
+  static constexpr int DT = D / 16;           // 16-wide output subtiles along D
+  static constexpr int PCH = 64 / Mma<T>::KC; // MFMA chunks along a 64-row block
+};
+
+// ROW image: 16-B chunk c of row r
+template <typename T, int D>
+__device__ __forceinline__ int row_off(int r, int c) {
+  constexpr int NCH = AT<T, D>::NCH;
+  constexpr int m = NCH >= 8 ? 7 : NCH - 1;
+  return r * AT<T, D>::RB + ((c ^ (r & m)) << 4);
+}
+// TR image: 16-B chunk c of row r (layout chosen for the transposed operand reads)
+template <typename T, int D>
+__device__ __forceinline__ int tr_chunk(int r, int c) {
+  if (sizeof(T) == 2) {
+    if (D == 64) return c ^ (2 * ((r >> 1) & 3));
+    return c ^ (2 * ((r >> 2) & 1));
+  }
+  return c ^ (4 * ((r >> 2) & 1));
+}
+
+// stage 64 rows [row0, row0+64) of a (token-strided) head slice into an image
+template <typename T, int D, bool TR>
+__device__ __forceinline__ void stage_rows(char* lds, const T* __restrict__ base, int64_t st, int64_t row0,
+                                           int64_t nrows, int tid) {
+  constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
+  for (int c = tid; c < 64 * NCH; c += 256) {
+    const int r = c / NCH, ch = c % NCH;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + r < nrows) v = *reinterpret_cast<const uint4*>(base + (row0 + r) * st + ch * EPC);
+    const int off = TR ? (r * AT<T, D>::RB + (tr_chunk<T, D>(r, ch) << 4)) : row_off<T, D>(r, ch);
+    *reinterpret_cast<uint4*>(lds + off) = v;
+  }
+}
+
+// A-operand fragment (16 rows starting at sub*16) from a ROW image, MFMA chunk kc along D
+template <typename T, int D>
+__device__ __forceinline__ uint4 row_frag(const char* lds, int sub, int kc, int lane) {
+  const int row = sub * 16 + (lane & 15);
+  return lds_read16(lds, row_off<T, D>(row, kc * 4 + (lane >> 4)));
+}
+
+// B-operand fragment from a TR image: k = rows of the 64-row block (split order for bf16),
+// n = 16 columns starting at dsub*16. chunk c covers rows [c*KC, c*KC+KC).
+template <typename T, int D>
+__device__ __forceinline__ uint4 tr_frag(const char* lds, int c, int dsub, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  constexpr int RB = AT<T, D>::RB;
+  if (sizeof(T) == 2) {
+    const int q = i >> 2, p = i & 3;
+    const int u = dsub * 4 + p;  // 8-B unit (4 bf16)
+    uint2 x[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = c * 32 + 16 * h + 4 * g + q;
+      const int ch = tr_chunk<T, D>(r, u >> 1);
+      x[h] = lds_read_tr16(lds + r * RB + (ch << 4) + ((u & 1) << 3));
+    }
+    return make_uint4(x[0].x, x[0].y, x[1].x, x[1].y);
+  } else {
+    const int col = dsub * 16 + i;
+    uint32_t v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int r = c * 16 + 4 * g + s;
+      const int ch = tr_chunk<T, D>(r, col >> 2);
+      v[s] = *reinterpret_cast<const uint32_t*>(lds + r * RB + (ch << 4) + (col & 3) * 4);
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// pack 16x16 accumulators (rows in split order) into the A fragment of MFMA chunk c
+template <typename T>
+__device__ __forceinline__ uint4 pack_acc(const f32x4* s, int c) {
+  if (sizeof(T) == 2) {
+    const f32x4 a = s[2 * c], b = s[2 * c + 1];
+    bf16x8 v = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+    return __builtin_bit_cast(uint4, v);
+  } else {
+    const f32x4 a = s[c];
+    return make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3]));
+  }
+}
+
+// per-lane 16-B operand chunks of one row (query or key) held in registers
+template <typename T, int D>
+__device__ __forceinline__ void load_row_regs(uint4* f, const T* __restrict__ base, int64_t st,
+                                              int64_t row, int64_t nrows, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int kc = 0; kc < AT<T, D>::KCH; ++kc) {
+    f[kc] = make_uint4(0, 0, 0, 0);
+    if (row < nrows) f[kc] = *reinterpret_cast<const uint4*>(base + row * st + (kc * 4 + g) * AT<T, D>::EPC);
+  }
+}
+
+__device__ __forceinline__ float bias_at(const AttnP& p, int64_t b, int64_t h, int64_t q, int64_t key) {
+  float v = 0.f;
+  if (p.key_bias) v += p.key_bias[b * p.Lk + key];
+  if (p.rel_bias) v += p.rel_bias[(h * p.Lq + q) * p.Lk + key];
+  return v;
+}
+
+// --------------------------------------------------------------------------------------------
+// forward
+// --------------------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* k_img = smem;
+  char* v_img = smem + C::TILE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
+  const int64_t myq = q0 + li;
+
+  uint4 qf[C::KCH];
+  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane);
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4 o[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t k0 = 0; k0 < p.Lk; k0 += 64) {
+    __syncthreads();
+    stage_rows<T, D, false>(k_img, kb, p.k_st, k0, p.Lk, tid);
+    stage_rows<T, D, true>(v_img, vb, p.v_st, k0, p.Lk, tid);
+    __syncthreads();
+
+    f32x4 s[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(k_img, ks, kc, lane), qf[kc]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t key = k0 + ks * 16 + 4 * g + r;
+        float v = s[ks][r] * p.scale;
+        if (key >= p.Lk) v = -INFINITY;
+        else if (p.key_bias || p.rel_bias) v += bias_at(p, b, h, myq < p.Lq ? myq : 0, key);
+        s[ks][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = __expf(m - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[ks][r] - mnew);
+        rs += e;
+        float pe = e;
+        if (p.p > 0.f) {
+          const int64_t key = k0 + ks * 16 + 4 * g + r;
+          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+          pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
+        }
+        s[ks][r] = pe;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    lsum = lsum * alpha + rs;
+    m = mnew;
+    // rescale O rows (row = local query 4g+r, whose alpha sits in lane 4g+r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
+    }
+#pragma unroll
+    for (int c = 0; c < C::PCH; ++c) {
+      const uint4 a = pack_acc<T>(s, c);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) Mma<T>::run(o[d], a, tr_frag<T, D>(v_img, c, d, lane));
+    }
+  }
+
+  T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float lr = __shfl(lsum, 4 * g + r, 64);
+    const int64_t q = q0 + 4 * g + r;
+    const float inv = 1.0f / lr;
+    if (q < p.Lq) {
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
+    }
+  }
+  if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = m + __logf(lsum);
+}
+
+// --------------------------------------------------------------------------------------------
+// backward: delta = rowsum(dO * O)
+// --------------------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ void attn_delta_kernel(AttnP p) {
+  // 8 lanes per (b,h,q) row for D=64 (4 for D=32): each lane a 16-B chunk
+  constexpr int LPR = AT<T, D>::NCH;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid / LPR;
+  const int ch = gid % LPR;
+  const int64_t total = p.B * p.H * p.Lq;
+  float s = 0.f;
+  if (row < total) {
+    const int64_t q = row % p.Lq, bh = row / p.Lq, b = bh / p.H, h = bh % p.H;
+    const T* o = reinterpret_cast<const T*>(p.o) + b * p.o_sb + q * p.o_st + h * D + ch * AT<T, D>::EPC;
+    const T* d = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + q * p.do_st + h * D + ch * AT<T, D>::EPC;
+#pragma unroll
+    for (int j = 0; j < AT<T, D>::EPC; ++j) s += to_f32(o[j]) * to_f32(d[j]);
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (row < total && ch == 0) p.delta[row] = s;
+}
+
+// --------------------------------------------------------------------------------------------
+// backward: dK, dV (workgroup = 64 keys, wave = 16 keys)
+// --------------------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* q_row = smem;
+  char* q_tr = smem + C::TILE;
+  char* do_row = smem + 2 * C::TILE;
+  char* do_tr = smem + 3 * C::TILE;
+  float* s_lse = reinterpret_cast<float*>(smem + 4 * C::TILE);
+  float* s_delta = s_lse + 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int64_t k0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const int64_t mykey = k0 + li;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * D;
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+
+  uint4 kf[C::KCH], vf[C::KCH];
+  load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane);
+  load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane);
+
+  f32x4 dk[C::DT], dv[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+
+  for (int64_t qs0 = 0; qs0 < p.Lq; qs0 += 64) {
+    __syncthreads();
+    stage_rows<T, D, false>(q_row, qb, p.q_st, qs0, p.Lq, tid);
+    stage_rows<T, D, true>(q_tr, qb, p.q_st, qs0, p.Lq, tid);
+    stage_rows<T, D, false>(do_row, dob, p.do_st, qs0, p.Lq, tid);
+    stage_rows<T, D, true>(do_tr, dob, p.do_st, qs0, p.Lq, tid);
+    if (tid < 64) {
+      const int64_t q = qs0 + tid;
+      s_lse[tid] = q < p.Lq ? p.lse[bh * p.Lq + q] : INFINITY;
+      s_delta[tid] = q < p.Lq ? p.delta[bh * p.Lq + q] : 0.f;
+    }
+    __syncthreads();
+
+    f32x4 pd[4], ds[4];
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) {
+        Mma<T>::run(sv, row_frag<T, D>(q_row, qs, kc, lane), kf[kc]);
+        Mma<T>::run(dp, row_frag<T, D>(do_row, qs, kc, lane), vf[kc]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lq = qs * 16 + 4 * g + r;
+        const int64_t q = qs0 + lq;
+        float pr = 0.f;
+        if (mykey < p.Lk) {
+          float sc = sv[r] * p.scale;
+          if ((p.key_bias || p.rel_bias) && q < p.Lq) sc += bias_at(p, b, h, q, mykey);
+          pr = __expf(sc - s_lse[lq]);
+        }
+        float z = 1.f;
+        if (p.p > 0.f) {
+          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + q) * p.Lk + mykey));
+          z = (hsh < p.thr) ? 0.f : p.keep_scale;
+        }
+        pd[qs][r] = pr * z;
+        ds[qs][r] = pr * (dp[r] * z - s_delta[lq]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C::PCH; ++c) {
+      const uint4 ap = pack_acc<T>(pd, c);
+      const uint4 as = pack_acc<T>(ds, c);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        Mma<T>::run(dv[d], ap, tr_frag<T, D>(do_tr, c, d, lane));
+        Mma<T>::run(dk[d], as, tr_frag<T, D>(q_tr, c, d, lane));
+      }
+    }
+  }
+
+  T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * D;
+  T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t key = k0 + 4 * g + r;
+    if (key < p.Lk) {
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        T* pk = dkb + key * p.dk_st + d * 16 + li;
+        T* pv = dvb + key * p.dv_st + d * 16 + li;
+        float vk = dk[d][r] * p.scale, vv = dv[d][r];
+        if (p.acc_dkv) { vk += to_f32(*pk); vv += to_f32(*pv); }
+        *pk = from_f32<T>(vk);
+        *pv = from_f32<T>(vv);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// backward: dQ (workgroup = 64 queries, wave = 16 queries)
+// --------------------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* k_row = smem;
+  char* k_tr = smem + C::TILE;
+  char* v_row = smem + 2 * C::TILE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const int64_t myq = q0 + li;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * D;
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+
+  uint4 qf[C::KCH], dof[C::KCH];
+  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane);
+  load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane);
+  const float lse = myq < p.Lq ? p.lse[bh * p.Lq + myq] : INFINITY;
+  const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+
+  f32x4 dq[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t k0 = 0; k0 < p.Lk; k0 += 64) {
+    __syncthreads();
+    stage_rows<T, D, false>(k_row, kb, p.k_st, k0, p.Lk, tid);
+    stage_rows<T, D, true>(k_tr, kb, p.k_st, k0, p.Lk, tid);
+    stage_rows<T, D, false>(v_row, vb, p.v_st, k0, p.Lk, tid);
+    __syncthreads();
+
+    f32x4 ds[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) {
+        Mma<T>::run(sv, row_frag<T, D>(k_row, ks, kc, lane), qf[kc]);
+        Mma<T>::run(dp, row_frag<T, D>(v_row, ks, kc, lane), dof[kc]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t key = k0 + ks * 16 + 4 * g + r;
+        float pr = 0.f;
+        if (key < p.Lk) {
+          float sc = sv[r] * p.scale;
+          if ((p.key_bias || p.rel_bias) && myq < p.Lq) sc += bias_at(p, b, h, myq, key);
+          pr = __expf(sc - lse);
+        }
+        float z = 1.f;
+        if (p.p > 0.f) {
+          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+          z = (hsh < p.thr) ? 0.f : p.keep_scale;
+        }
+        ds[ks][r] = pr * (dp[r] * z - dlt);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C::PCH; ++c) {
+      const uint4 as = pack_acc<T>(ds, c);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) Mma<T>::run(dq[d], as, tr_frag<T, D>(k_tr, c, d, lane));
+    }
+  }
+
+  T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t q = q0 + 4 * g + r;
+    if (q < p.Lq) {
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        T* pq = dqb + q * p.dq_st + d * 16 + li;
+        float vq = dq[d][r] * p.scale;
+        if (p.acc_dq) vq += to_f32(*pq);
+        *pq = from_f32<T>(vq);
+      }
+    }
+  }
+}
+
+int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
+  MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "attn: bad dtype");
+  MMFD_CHECK_ARG(a.D == 32 || a.D == 64, "attn: head_dim %lld unsupported (32 or 64)", (long long)a.D);
+  MMFD_CHECK_ARG(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attn: bad shape");
+  MMFD_CHECK_ARG(a.q && a.k && a.v && a.o && a.lse, "attn: null pointer");
+  const int epc = a.dtype == MMFD_BF16 ? 8 : 4;
+  auto al = [&](const void* ptr, int64_t sb, int64_t st) {
+    return ((uintptr_t)ptr & 15) == 0 && sb % epc == 0 && st % epc == 0;
+  };
+  MMFD_CHECK_ARG(al(a.q, a.q_sb, a.q_st) && al(a.k, a.k_sb, a.k_st) && al(a.v, a.v_sb, a.v_st),
+                 "attn: q/k/v must be 16-B aligned with strides multiple of 16 B");
+  MMFD_CHECK_ARG(a.dropout_p <= 0.f || a.seed, "attn: dropout needs seed");
+  MMFD_CHECK_ARG(a.dropout_p < 1.f, "attn: dropout p must be < 1");
+  if (bwd) {
+    MMFD_CHECK_ARG(a.dout && a.dq && a.dk && a.dv && a.delta, "attn_bwd: null pointer");
+    MMFD_CHECK_ARG(al(a.dout, a.do_sb, a.do_st), "attn_bwd: dout alignment");
+    MMFD_CHECK_ARG(a.d_rel_bias == nullptr, "attn_bwd: relative-bias gradient not supported");
+  }
+  p.B = a.B; p.H = a.H; p.Lq = a.Lq; p.Lk = a.Lk; p.scale = a.scale;
+  p.q = a.q; p.q_sb = a.q_sb; p.q_st = a.q_st;
+  p.k = a.k; p.k_sb = a.k_sb; p.k_st = a.k_st;
+  p.v = a.v; p.v_sb = a.v_sb; p.v_st = a.v_st;
+  p.o = a.o; p.o_sb = a.o_sb; p.o_st = a.o_st;
+  p.lse = a.lse; p.key_bias = a.key_bias; p.rel_bias = a.rel_bias;
+  p.p = a.dropout_p > 0.f ? a.dropout_p : 0.f; p.thr = mmfd_drop_threshold(p.p);
+  p.keep_scale = 1.0f / (1.0f - p.p); p.seed = a.seed; p.salt = a.salt;
+  p.dout = a.dout; p.do_sb = a.do_sb; p.do_st = a.do_st;
+  p.dq = a.dq; p.dq_sb = a.dq_sb; p.dq_st = a.dq_st;
+  p.dk = a.dk; p.dk_sb = a.dk_sb; p.dk_st = a.dk_st;
+  p.dv = a.dv; p.dv_sb = a.dv_sb; p.dv_st = a.dv_st;
+  p.delta = a.delta;
+  p.acc_dq = a.accumulate_dq; p.acc_dkv = a.accumulate_dkv;
+  return 0;
+}
+
+template <typename T, int D>
+void launch_fwd(const AttnP& p, hipStream_t s) {
+  dim3 grid((unsigned)((p.Lq + 63) / 64), (unsigned)(p.B * p.H));
+  constexpr int lds = 2 * AT<T, D>::TILE;
+  hipLaunchKernelGGL((attn_fwd_kernel<T, D>), grid, dim3(256), lds, s, p);
+}
+template <typename T, int D>
+void launch_bwd(const AttnP& p, hipStream_t s) {
+  const int64_t rows = p.B * p.H * p.Lq;
+  constexpr int nch = AT<T, D>::NCH;
+  constexpr int lds1 = 4 * AT<T, D>::TILE + 512;
+  constexpr int lds2 = 3 * AT<T, D>::TILE;
+  const int64_t threads = rows * nch;
+  hipLaunchKernelGGL((attn_delta_kernel<T, D>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, p);
+  dim3 g1((unsigned)((p.Lk + 63) / 64), (unsigned)(p.B * p.H));
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, D>), g1, dim3(256), lds1, s, p);
+  dim3 g2((unsigned)((p.Lq + 63) / 64), (unsigned)(p.B * p.H));
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D>), g2, dim3(256), lds2, s, p);
+}
+
+}  // namespace
+
+extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(a != nullptr, "attn_fwd: null args");
+  AttnP p;
+  int rc = fill(*a, p, false);
+  if (rc) return rc;
+  if (p.B == 0 || p.Lq == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dtype == MMFD_BF16) { if (a->D == 64) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
+  else { if (a->D == 64) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
+  MMFD_CHECK_LAUNCH("attn_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(a != nullptr, "attn_bwd: null args");
+  AttnP p;
+  int rc = fill(*a, p, true);
+  if (rc) return rc;
+  if (p.B == 0 || p.Lq == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dtype == MMFD_BF16) { if (a->D == 64) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
+  else { if (a->D == 64) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
+  MMFD_CHECK_LAUNCH("attn_bwd");
+  return 0;
+}

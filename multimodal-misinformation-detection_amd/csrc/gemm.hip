@@ -1,0 +1,440 @@
+// MFMA GEMM with fused epilogue for gfx950.
+//
+// Tile 128x128, 256 threads = 4 waves (2x2), each wave owns 64x64 = 4x4 tiles of the 16x16 MFMA.
+// K is staged 128 bytes per tile row (64 bf16 / 32 fp32) through a double-buffered LDS image
+// (register staging: global loads for tile t+1 are issued before the MFMAs of tile t and written
+// to the other buffer after them, one barrier per K tile).
+//
+// Operand layouts (template TA / TB):
+//   0 = "K-contiguous" (A[m][k], or B[n][k] = nn.Linear weight): LDS image [128 rows][128 B],
+//       16-B chunk c of row r stored at chunk c ^ (r & 7) (conflict-free ds_read_b128);
+//   1 = "MN-contiguous" (A[k][m] or B[k][n]): LDS image [BK rows][128 elements]; bf16 fragments
+//       come from ds_read_b64_tr_b16 (hardware transpose), fp32 fragments from 4 ds_read_b32.
+// The three nn.Linear products are (TA,TB) = (0,0) forward, (0,1) grad-input, (1,1) grad-weight.
+#include "common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int BM = 128, BN = 128, ROWB = 128, NT = 256;
+constexpr int TILE_BYTES = 16384;  // one operand tile, any layout / dtype
+
+template <typename T> struct GT {
+  static constexpr int ESZ = sizeof(T);
+  static constexpr int BK = ROWB / ESZ;      // K per tile
+  static constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
+  static constexpr int KCH = BK / Mma<T>::KC; // MFMA chunks per tile (2)
+  static constexpr int MN_ROWB = 128 * ESZ;  // bytes per k-row of an MN-contiguous image
+  static constexpr int MN_CPR = MN_ROWB / 16;
+};
+
+struct EpiArgs {
+  const float* bias;
+  const void* residual; int64_t ldr;
+  void* aux; int64_t ldaux;
+  int act;
+  float p; uint32_t thr; float keep_scale;
+  const uint64_t* seed; uint64_t salt;
+  float beta;
+};
+
+template <typename TC>
+__device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t ldc, int64_t N,
+                                               int64_t row, int64_t col, float z, uint64_t seed) {
+  if (e.bias) z += e.bias[col];
+  if (e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU) {
+    if (e.aux) reinterpret_cast<TC*>(e.aux)[row * e.ldaux + col] = from_f32<TC>(z);
+    z = (e.act == MMFD_ACT_GELU) ? gelu_f(z) : fmaxf(z, 0.0f);
+  } else if (e.act == MMFD_ACT_GELU_BWD) {
+    z *= gelu_grad_f(to_f32(reinterpret_cast<const TC*>(e.aux)[row * e.ldaux + col]));
+  } else if (e.act == MMFD_ACT_RELU_BWD) {
+    z = (to_f32(reinterpret_cast<const TC*>(e.aux)[row * e.ldaux + col]) > 0.0f) ? z : 0.0f;
+  }
+  if (e.p > 0.0f) {
+    const uint32_t h = mmfd_hash(seed, e.salt, (uint64_t)row * (uint64_t)N + (uint64_t)col);
+    z = (h < e.thr) ? 0.0f : z * e.keep_scale;
+  }
+  if (e.residual) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
+  TC* cp = C + row * ldc + col;
+  if (e.beta != 0.0f) z += e.beta * to_f32(*cp);
+  *cp = from_f32<TC>(z);
+}
+
+// --------------------------------------------------------------------------------------------
+// operand staging
+// --------------------------------------------------------------------------------------------
+template <typename T, int LAYOUT>
+struct Stage {
+  // 4 x 16-byte chunks per thread per tile
+  uint4 r[4];
+
+  __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int64_t mn0, int64_t mn_ext,
+                                       int64_t k0, int64_t K, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      int64_t row, col;  // row index in the stored matrix, column (elements)
+      bool ok;
+      if (LAYOUT == 0) {
+        const int tr = c >> 3, kc = c & 7;
+        row = mn0 + tr; col = k0 + (int64_t)kc * GT<T>::EPC;
+        ok = (row < mn_ext) && (col < K);
+      } else {
+        const int tr = c / GT<T>::MN_CPR, cc = c % GT<T>::MN_CPR;
+        row = k0 + tr; col = mn0 + (int64_t)cc * GT<T>::EPC;
+        ok = (row < K) && (col < mn_ext);
+      }
+      if (ok) r[i] = *reinterpret_cast<const uint4*>(p + row * ld + col);
+      else r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      int off;
+      if (LAYOUT == 0) {
+        const int tr = c >> 3, kc = c & 7;
+        off = tr * ROWB + ((kc ^ (tr & 7)) << 4);
+      } else {
+        const int tr = c / GT<T>::MN_CPR, cc = c % GT<T>::MN_CPR;
+        int sc;
+        if (sizeof(T) == 2) sc = cc ^ (2 * ((tr & 3) | (((tr >> 3) & 1) << 2)));
+        else sc = cc ^ (4 * ((tr >> 2) & 1));
+        off = tr * GT<T>::MN_ROWB + (sc << 4);
+      }
+      *reinterpret_cast<uint4*>(lds + off) = r[i];
+    }
+  }
+};
+
+// fragment of 16 rows (K-contig) / 16 columns (MN-contig) for MFMA chunk kc
+template <typename T, int LAYOUT>
+__device__ __forceinline__ uint4 load_frag(const char* lds, int sub, int kc, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  if (LAYOUT == 0) {
+    const int row = sub * 16 + i;
+    const int c = kc * 4 + g;
+    return lds_read16(lds, row * ROWB + ((c ^ (row & 7)) << 4));
+  } else if (sizeof(T) == 2) {
+    const int q = i >> 2, p = i & 3;
+    const int r1 = kc * 32 + 8 * g + q, r2 = r1 + 4;
+    const int u = sub * 4 + p;
+    const int f1 = 4 * ((r1 & 3) | (((r1 >> 3) & 1) << 2));
+    const int f2 = 4 * ((r2 & 3) | (((r2 >> 3) & 1) << 2));
+    const uint2 a = lds_read_tr16(lds + r1 * 256 + ((u ^ f1) << 3));
+    const uint2 b = lds_read_tr16(lds + r2 * 256 + ((u ^ f2) << 3));
+    return make_uint4(a.x, a.y, b.x, b.y);
+  } else {
+    const int col = sub * 16 + i;
+    const int ch = col >> 2, w = (col & 3) * 4;
+    uint32_t v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = kc * 16 + 4 * g + s;
+      const int sc = ch ^ (4 * ((row >> 2) & 1));
+      v[s] = *reinterpret_cast<const uint32_t*>(lds + row * 512 + (sc << 4) + w);
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <typename T, int TA, int TB, typename TC>
+__global__ void __launch_bounds__(NT, 2)
+gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                 TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
+                 int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // buffer b: A image at smem + 2*b*TILE_BYTES, B image right after it
+#define LDS_A(b) (smem + (b) * 2 * TILE_BYTES)
+#define LDS_B(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int lin = blockIdx.y * gx + blockIdx.x;
+  const int tile = xcd_remap(lin, gx * gy);
+  const int tm = tile / gx, tn = tile % gx;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  const int nkt_total = (int)((K + GT<T>::BK - 1) / GT<T>::BK);
+  const int kt0 = blockIdx.z * tiles_per_split;
+  const int kt1 = min(nkt_total, kt0 + tiles_per_split);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<T, TA> sa;
+  Stage<T, TB> sb;
+  if (kt0 < kt1) {
+    sa.load(A, lda, m0, M, (int64_t)kt0 * GT<T>::BK, K, tid);
+    sb.load(B, ldb, n0, N, (int64_t)kt0 * GT<T>::BK, K, tid);
+    sa.store(LDS_A(0), tid);
+    sb.store(LDS_B(0), tid);
+  }
+  __syncthreads();
+
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = (kt + 1) < kt1;
+    if (more) {
+      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * GT<T>::BK, K, tid);
+      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * GT<T>::BK, K, tid);
+    }
+    const char* la = LDS_A(cur);
+    const char* lb = LDS_B(cur);
+#pragma unroll
+    for (int kc = 0; kc < GT<T>::KCH; ++kc) {
+      uint4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = load_frag<T, TA>(la, wm * 4 + i, kc, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = load_frag<T, TB>(lb, wn * 4 + j, kc, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+    }
+    if (more) {
+      sa.store(LDS_A(cur ^ 1), tid);
+      sb.store(LDS_B(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+#undef LDS_A
+#undef LDS_B
+  const int g = lane >> 4, ci = lane & 15;
+  if (ws) {
+    float* slab = ws + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * 64 + j * 16 + ci;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm * 64 + i * 16 + 4 * g + r;
+          if (row < M && col < N) slab[row * N + col] = alpha * acc[i][j][r];
+        }
+      }
+    return;
+  }
+  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 16 + ci;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + 4 * g + r;
+        if (row < M && col < N) epilogue_store<TC>(e, C, ldc, N, row, col, alpha * acc[i][j][r], seed);
+      }
+    }
+}
+
+template <typename TC>
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
+                                     int64_t ldc, int64_t M, int64_t N, EpiArgs e) {
+  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+  const int64_t total = M * N;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float z = 0.f;
+    for (int s = 0; s < splits; ++s) z += ws[(int64_t)s * total + idx];
+    epilogue_store<TC>(e, C, ldc, N, idx / N, idx % N, z, seed);
+  }
+}
+
+// Plain FMA GEMM for shapes the MFMA path cannot take (tiny / unaligned: classifier heads).
+template <typename T, typename TC>
+__global__ void gemm_simple_kernel(const T* __restrict__ A, int64_t lda, int ta, const T* __restrict__ B,
+                                   int64_t ldb, int tb, TC* __restrict__ C, int64_t ldc, int64_t M,
+                                   int64_t N, int64_t K, float alpha, EpiArgs e) {
+  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+  const int64_t total = M * N;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = idx / N, n = idx % N;
+    float s = 0.f;
+    for (int64_t k = 0; k < K; ++k) {
+      const float a = to_f32(ta ? A[k * lda + m] : A[m * lda + k]);
+      const float b = to_f32(tb ? B[k * ldb + n] : B[n * ldb + k]);
+      s = fmaf(a, b, s);
+    }
+    epilogue_store<TC>(e, C, ldc, N, m, n, alpha * s, seed);
+  }
+}
+
+template <typename T, int TA, int TB, typename TC>
+void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps,
+                 hipStream_t s) {
+  dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
+  hipLaunchKernelGGL((gemm_mfma_kernel<T, TA, TB, TC>), grid, dim3(NT), 4 * TILE_BYTES, s,
+                     (const T*)a.A, a.lda, (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K,
+                     a.alpha, tps, e);
+}
+
+template <typename T, typename TC>
+void dispatch_layout(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps,
+                     hipStream_t s) {
+  if (!a.trans_a && !a.trans_b) launch_mfma<T, 0, 0, TC>(a, e, ws, splits, tps, s);
+  else if (!a.trans_a && a.trans_b) launch_mfma<T, 0, 1, TC>(a, e, ws, splits, tps, s);
+  else if (a.trans_a && !a.trans_b) launch_mfma<T, 1, 0, TC>(a, e, ws, splits, tps, s);
+  else launch_mfma<T, 1, 1, TC>(a, e, ws, splits, tps, s);
+}
+
+bool mfma_ok(const mmfd_gemm_args& a) {
+  const int epc = (a.dtype == MMFD_BF16) ? 8 : 4;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(a.A) || !al16(a.B)) return false;
+  if (a.lda % epc || a.ldb % epc) return false;
+  const int64_t a_ext = a.trans_a ? a.M : a.K;  // contiguous extent
+  const int64_t b_ext = a.trans_b ? a.N : a.K;
+  if (a_ext % epc || b_ext % epc) return false;
+  if (a.M < 16 || a.N < 16 || a.K < 16) return false;
+  return true;
+}
+
+int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
+  const int T = (a.dtype == MMFD_BF16) ? 64 : 32;
+  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int64_t nkt = (a.K + T - 1) / T;
+  int splits = 1;
+  if (a.splits > 0) splits = a.splits;
+  else if (tiles < 240 && nkt >= 16) {
+    splits = (int)((512 + tiles - 1) / tiles);
+    splits = (int)std::min<int64_t>(splits, nkt / 8);
+    splits = std::min(splits, 16);
+    if (splits < 1) splits = 1;
+  }
+  if (splits > nkt) splits = (int)nkt;
+  if (splits < 1) splits = 1;
+  *ws_bytes_needed = (splits > 1) ? (int64_t)splits * a.M * a.N * 4 : 0;
+  return splits;
+}
+
+}  // namespace
+
+extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
+  if (!a || !mfma_ok(*a)) return 0;
+  int64_t need = 0;
+  choose_splits(*a, &need);
+  return need;
+}
+
+extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(ap != nullptr, "mmfd_gemm: null args");
+  const mmfd_gemm_args& a = *ap;
+  hipStream_t s = (hipStream_t)stream;
+  MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "mmfd_gemm: bad dtype %d", a.dtype);
+  MMFD_CHECK_ARG(a.c_dtype == MMFD_F32 || a.c_dtype == MMFD_BF16, "mmfd_gemm: bad c_dtype %d", a.c_dtype);
+  MMFD_CHECK_ARG(a.M >= 0 && a.N >= 0 && a.K >= 0, "mmfd_gemm: negative shape");
+  MMFD_CHECK_ARG(a.C != nullptr, "mmfd_gemm: null C");
+  MMFD_CHECK_ARG(a.ldc >= a.N, "mmfd_gemm: ldc %lld < N %lld", (long long)a.ldc, (long long)a.N);
+  const int act = a.ep.act;
+  MMFD_CHECK_ARG(act >= 0 && act <= 4, "mmfd_gemm: bad act %d", act);
+  MMFD_CHECK_ARG(!(act >= MMFD_ACT_GELU_BWD) || a.ep.aux != nullptr, "mmfd_gemm: backward act needs aux");
+  MMFD_CHECK_ARG(a.ep.dropout_p <= 0.f || a.ep.seed != nullptr, "mmfd_gemm: dropout needs seed");
+  MMFD_CHECK_ARG(a.ep.dropout_p < 1.f, "mmfd_gemm: dropout p must be < 1");
+  if (a.M == 0 || a.N == 0) return 0;
+  MMFD_CHECK_ARG(a.K == 0 || (a.A && a.B), "mmfd_gemm: null operand");
+
+  EpiArgs e;
+  e.bias = a.ep.bias; e.residual = a.ep.residual; e.ldr = a.ep.ldr; e.aux = a.ep.aux;
+  e.ldaux = a.ep.ldaux; e.act = act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
+  e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
+  e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta;
+
+  const bool bf = a.dtype == MMFD_BF16, cbf = a.c_dtype == MMFD_BF16;
+  if (!mfma_ok(a)) {
+    const int64_t total = a.M * a.N;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+#define SIMPLE(T, TC)                                                                          \
+  hipLaunchKernelGGL((gemm_simple_kernel<T, TC>), dim3(blocks), dim3(256), 0, s, (const T*)a.A, \
+                     a.lda, a.trans_a, (const T*)a.B, a.ldb, a.trans_b, (TC*)a.C, a.ldc, a.M, a.N, \
+                     a.K, a.alpha, e)
+    if (bf) { if (cbf) SIMPLE(bf16, bf16); else SIMPLE(bf16, float); }
+    else { if (cbf) SIMPLE(float, bf16); else SIMPLE(float, float); }
+#undef SIMPLE
+    MMFD_CHECK_LAUNCH("gemm_simple");
+    return 0;
+  }
+
+  int64_t need = 0;
+  int splits = choose_splits(a, &need);
+  if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need)) {
+    // shrink to what the workspace allows
+    const int64_t per = a.M * a.N * 4;
+    int fit = (a.workspace && per > 0) ? (int)std::min<int64_t>(a.workspace_bytes / per, 16) : 1;
+    splits = fit > 1 ? std::min(splits, fit) : 1;
+  }
+  const int T = bf ? 64 : 32;
+  const int nkt = (int)((a.K + T - 1) / T);
+  const int tps = (nkt + splits - 1) / std::max(splits, 1);
+  splits = tps > 0 ? (nkt + tps - 1) / tps : 1;
+  if (splits < 1) splits = 1;
+  float* ws = splits > 1 ? (float*)a.workspace : nullptr;
+
+  if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
+  else { if (cbf) dispatch_layout<float, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<float, float>(a, e, ws, splits, tps, s); }
+  MMFD_CHECK_LAUNCH("gemm_mfma");
+  if (ws) {
+    const int64_t total = a.M * a.N;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc, a.M, a.N, e);
+    else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc, a.M, a.N, e);
+    MMFD_CHECK_LAUNCH("splitk_reduce");
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// column sums (bias gradients), deterministic two-pass
+// ------------------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int64_t N,
+                                      int64_t rows_per_block, float* __restrict__ part) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += to_f32(X[r * ldx + col]);
+  part[(int64_t)blockIdx.y * N + col] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int64_t N,
+                                    float* __restrict__ out, float beta) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * N + col];
+  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + s;
+}
+}  // namespace
+
+extern "C" int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, float* out,
+                           float beta, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MMFD_CHECK_ARG(dtype == MMFD_F32 || dtype == MMFD_BF16, "mmfd_colsum: bad dtype");
+  if (N == 0) return 0;
+  int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, M / 64));
+  if (workspace_bytes < (int64_t)nparts * N * 4) nparts = (int)(workspace_bytes / (N * 4));
+  MMFD_CHECK_ARG(nparts >= 1 && workspace, "mmfd_colsum: workspace too small");
+  const int64_t rpb = (M + nparts - 1) / nparts;
+  dim3 g1((unsigned)((N + 255) / 256), (unsigned)nparts);
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((colsum_partial_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)X, ldx, M, N, rpb, (float*)workspace);
+  else
+    hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)X, ldx, M, N, rpb, (float*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s,
+                     (const float*)workspace, nparts, N, out, beta);
+  MMFD_CHECK_LAUNCH("colsum");
+  return 0;
+}

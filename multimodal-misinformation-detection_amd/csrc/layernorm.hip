@@ -1,0 +1,225 @@
+// LayerNorm forward / backward (one wave per row, width <= 1024, width % 4 == 0).
+// Replaces nn.LayerNorm in the fusion head (model.py:39-46, 155-162; eps 1e-5) and the BERT/ViT
+// LayerNorms (eps 1e-12). Statistics in fp32; gamma/beta gradients via a deterministic two-pass
+// column reduction (per-lane column ownership -> per-block partials -> final sum).
+#include "common.h"
+#include <algorithm>
+
+namespace {
+constexpr int MAXC = 4;  // 4-element chunks per lane -> width <= 1024
+
+template <typename T> struct V4;
+template <> struct V4<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(p); v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct V4<bf16> {
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[4]) {
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float (&v)[4]) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+    b4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, o);
+  }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, int width, const T* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float eps, T* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = width >> 2;
+  float v[MAXC][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      V4<T>::load(x + row * ldx + 4 * c, v[j]);
+      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+    }
+  }
+  const float mu = wave_sum(s) / (float)width;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[j][e] - mu; q += d * d; }
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)width + eps);
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      const float4 gg = *reinterpret_cast<const float4*>(gamma + 4 * c);
+      const float4 bb = *reinterpret_cast<const float4*>(beta + 4 * c);
+      float o[4];
+      o[0] = (v[j][0] - mu) * rs * gg.x + bb.x;
+      o[1] = (v[j][1] - mu) * rs * gg.y + bb.y;
+      o[2] = (v[j][2] - mu) * rs * gg.z + bb.z;
+      o[3] = (v[j][3] - mu) * rs * gg.w + bb.w;
+      V4<T>::store(y + row * ldy + 4 * c, o);
+    }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, int width, const T* __restrict__ dy, int64_t lddy,
+                                                     const T* __restrict__ x, int64_t ldx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     T* __restrict__ dx, int64_t lddx, const T* __restrict__ dx_add,
+                                                     int64_t ldadd, T* __restrict__ dx_drop, float p, uint32_t thr,
+                                                     const uint64_t* __restrict__ seedp, uint64_t salt,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = width >> 2;
+  const uint64_t seed = (dx_drop && p > 0.f) ? *seedp : 0ull;
+  const float keep = 1.0f / (1.0f - p);
+  float pg[MAXC][4], pb[MAXC][4];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { pg[j][e] = 0.f; pb[j][e] = 0.f; }
+
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXC][4], g[MAXC][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        float d[4], xv[4];
+        V4<T>::load(dy + row * lddy + 4 * c, d);
+        V4<T>::load(x + row * ldx + 4 * c, xv);
+        const float4 gg = *reinterpret_cast<const float4*>(gamma + 4 * c);
+        const float gv[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[j][e] = (xv[e] - mu) * rs;
+          g[j][e] = d[e] * gv[e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+          pg[j][e] += d[e] * xh[j][e];
+          pb[j][e] += d[e];
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / (float)width;
+    const float c2 = wave_sum(s2) / (float)width;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        float o[4], add[4] = {0.f, 0.f, 0.f, 0.f};
+        if (dx_add) V4<T>::load(dx_add + row * ldadd + 4 * c, add);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (g[j][e] - c1 - xh[j][e] * c2) + add[e];
+        V4<T>::store(dx + row * lddx + 4 * c, o);
+        if (dx_drop) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t h = mmfd_hash(seed, salt, (uint64_t)row * (uint64_t)width + 4 * c + e);
+            o[e] = (p > 0.f && h < thr) ? 0.f : o[e] * (p > 0.f ? keep : 1.f);
+          }
+          V4<T>::store(dx_drop + row * lddx + 4 * c, o);
+        }
+      }
+    }
+  }
+  // block reduction of the per-lane column partials: chunk c = lane + 64 j, handled 256 cols at a time
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    if (64 * j >= nch) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[wave][0][lane * 4 + e] = pg[j][e];
+      red[wave][1][lane * 4 + e] = pb[j][e];
+    }
+    __syncthreads();
+    const int col_local = threadIdx.x;  // 0..255 within this 256-column slab
+    const int col = 256 * j + col_local;
+    if (col < width) {
+      const float sg = red[0][0][col_local] + red[1][0][col_local] + red[2][0][col_local] + red[3][0][col_local];
+      const float sb = red[0][1][col_local] + red[1][1][col_local] + red[2][1][col_local] + red[3][1][col_local];
+      part[((int64_t)blockIdx.x * 2 + 0) * width + col] = sg;
+      part[((int64_t)blockIdx.x * 2 + 1) * width + col] = sb;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void ln_bwd_final_kernel(const float* __restrict__ part, int nparts, int width, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, float beta_acc) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= width) return;
+  float sg = 0.f, sb = 0.f;
+  for (int b = 0; b < nparts; ++b) {
+    sg += part[((int64_t)b * 2 + 0) * width + col];
+    sb += part[((int64_t)b * 2 + 1) * width + col];
+  }
+  if (dgamma) dgamma[col] = (beta_acc != 0.f ? beta_acc * dgamma[col] : 0.f) + sg;
+  if (dbeta) dbeta[col] = (beta_acc != 0.f ? beta_acc * dbeta[col] : 0.f) + sb;
+}
+}  // namespace
+
+extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
+                                  const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
+                                  float* mean, float* rstd, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(width > 0 && width <= 1024 && width % 4 == 0, "layernorm: width %lld unsupported", (long long)width);
+  MMFD_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: leading dims must be multiples of 4");
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+  MMFD_CHECK_LAUNCH("layernorm_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
+                                  const void* x, int64_t ldx, const float* gamma, const float* mean,
+                                  const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
+                                  float* dgamma, float* dbeta, float beta_acc, void* dx_drop,
+                                  float dropout_p, const uint64_t* seed, uint64_t salt,
+                                  void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(width > 0 && width <= 1024 && width % 4 == 0, "layernorm_bwd: width %lld unsupported", (long long)width);
+  MMFD_CHECK_ARG(!(dx_drop && dropout_p > 0.f) || seed, "layernorm_bwd: dropout needs seed");
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  int nblocks = (int)std::min<int64_t>((rows + 3) / 4, 512);
+  const int64_t per = 2 * width * 4;
+  if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
+  MMFD_CHECK_ARG(nblocks >= 1 && workspace, "layernorm_bwd: workspace too small");
+  const float p = dropout_p > 0.f ? dropout_p : 0.f;
+  const uint32_t thr = mmfd_drop_threshold(p);
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
+                       (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd, (bf16*)dx_drop,
+                       p, thr, seed, salt, (float*)workspace);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const float*)dy, lddy,
+                       (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx, (const float*)dx_add, ldadd,
+                       (float*)dx_drop, p, thr, seed, salt, (float*)workspace);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(ln_bwd_final_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, s, (const float*)workspace,
+                       nblocks, (int)width, dgamma, dbeta, beta_acc);
+  MMFD_CHECK_LAUNCH("layernorm_bwd");
+  return 0;
+}

@@ -1,0 +1,390 @@
+// Memory-bound kernels on the training path: sequence mean pooling, summed cross entropy,
+// BERT embeddings (+LayerNorm), ViT patchify / token assembly, multi-tensor AdamW.
+#include "common.h"
+#include <algorithm>
+#include <math.h>
+
+namespace {
+inline unsigned gridn(int64_t n, int per) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, 16384));
+}
+
+// ---------------------------------------------------------------------------------------------
+// mean over the sequence dim: x [B][L][D] -> out [B][ldo]  (model.py:332 `S.mean(dim=1)`)
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void seq_mean_fwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ x, T* __restrict__ out,
+                                    int64_t ldo) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B * D; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / D, d = i % D;
+    const T* p = x + b * L * D + d;
+    float s = 0.f;
+    for (int64_t l = 0; l < L; ++l) s += to_f32(p[l * D]);
+    out[b * ldo + d] = from_f32<T>(s / (float)L);
+  }
+}
+template <typename T>
+__global__ void seq_mean_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dout, int64_t ldo,
+                                    T* __restrict__ dx) {
+  const float inv = 1.0f / (float)L;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B * L * D; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = i % D, b = i / (L * D);
+    dx[i] = from_f32<T>(to_f32(dout[b * ldo + d]) * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// summed cross entropy over paths; one block, rows = n_paths * B
+// ---------------------------------------------------------------------------------------------
+__global__ void xent_kernel(int n_paths, int64_t B, int64_t C, const float* const* __restrict__ logits,
+                            const int64_t* __restrict__ labels, int64_t label_ld, float* __restrict__ loss,
+                            float* const* __restrict__ dlogits, const float* __restrict__ dscale) {
+  __shared__ float red[4][256];
+  const float sc = dscale ? *dscale : 1.0f;
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t rr = threadIdx.x; rr < (int64_t)n_paths * B; rr += blockDim.x) {
+    const int path = (int)(rr / B);
+    const int64_t b = rr % B;
+    const float* z = logits[path] + b * C;
+    float mx = -INFINITY;
+    for (int64_t c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
+    float se = 0.f;
+    for (int64_t c = 0; c < C; ++c) se += expf(z[c] - mx);
+    const float lse = mx + logf(se);
+    const int64_t y = labels[b * label_ld + path];
+    part[path] += lse - z[y];
+    if (dlogits) {
+      float* dz = dlogits[path] + b * C;
+      for (int64_t c = 0; c < C; ++c) dz[c] = (expf(z[c] - lse) - (c == y ? 1.f : 0.f)) * sc / (float)B;
+    }
+  }
+  for (int p = 0; p < 4; ++p) red[p][threadIdx.x] = part[p];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int p = 0; p < 4; ++p) red[p][threadIdx.x] += red[p][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int p = 0; p < n_paths; ++p) {
+      const float lp = red[p][0] / (float)B;
+      loss[1 + p] = lp;
+      tot += lp;
+    }
+    loss[0] = tot;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BERT embeddings: sum = word[id] + pos[t] + type[tt]; y = dropout(LN(sum))   (wave per token)
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) embed_ln_fwd_kernel(int64_t B, int64_t L, int64_t D, const int64_t* __restrict__ ids,
+                                                           const int64_t* __restrict__ tts, const float* __restrict__ word,
+                                                           const float* __restrict__ pos, const float* __restrict__ type,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           float eps, T* __restrict__ sum_out, T* __restrict__ y,
+                                                           float* __restrict__ mean, float* __restrict__ rstd, float p,
+                                                           uint32_t thr, const uint64_t* __restrict__ seedp, uint64_t salt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B * L) return;
+  const int64_t t = row % L;
+  const int64_t id = ids[row];
+  const int64_t tt = tts ? tts[row] : 0;
+  constexpr int MAXV = 16;  // D <= 1024
+  float v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int64_t d = lane + 64 * j;
+    v[j] = 0.f;
+    if (d < D) {
+      float e = word[id * D + d] + pos[t * D + d] + type[tt * D + d];
+      e = to_f32(from_f32<T>(e));  // the stored sum is what the backward LayerNorm re-reads
+      sum_out[row * D + d] = from_f32<T>(e);
+      v[j] = e;
+      s += e;
+    }
+  }
+  const float mu = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int64_t d = lane + 64 * j;
+    if (d < D) q += (v[j] - mu) * (v[j] - mu);
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)D + eps);
+  const uint64_t seed = p > 0.f ? *seedp : 0ull;
+  const float keep = 1.0f / (1.0f - p);
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int64_t d = lane + 64 * j;
+    if (d < D) {
+      float o = (v[j] - mu) * rs * gamma[d] + beta[d];
+      if (p > 0.f) {
+        const uint32_t h = mmfd_hash(seed, salt, (uint64_t)(row * D + d));
+        o = (h < thr) ? 0.f : o * keep;
+      }
+      y[row * D + d] = from_f32<T>(o);
+    }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+template <typename T>
+__global__ void embed_word_bwd_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ ids, const T* __restrict__ dsum,
+                                      float* __restrict__ dword, int64_t padding_idx) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
+    const int64_t id = ids[row];
+    if (id == padding_idx) continue;
+    for (int64_t d = lane; d < D; d += 64) atomicAdd(dword + id * D + d, to_f32(dsum[row * D + d]));
+  }
+}
+// dpos[t][d] = sum_b dsum[b][t][d]; type grads per token type (0/1) via column partials
+template <typename T>
+__global__ void embed_pos_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dsum, float* __restrict__ dpos) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L * D; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t b = 0; b < B; ++b) s += to_f32(dsum[b * L * D + i]);
+    dpos[i] += s;
+  }
+}
+template <typename T>
+__global__ void embed_type_bwd_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ tts, const T* __restrict__ dsum,
+                                      float* __restrict__ dtype_emb) {
+  // block = 256 columns x one row-slab; two accumulators (token types 0 and 1), fp32 atomics per block
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = std::min<int64_t>(rows, r0 + per);
+  float s0 = 0.f, s1 = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float g = to_f32(dsum[r * D + d]);
+    if (tts && tts[r] == 1) s1 += g; else s0 += g;
+  }
+  atomicAdd(dtype_emb + d, s0);
+  atomicAdd(dtype_emb + D + d, s1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// ViT
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void patchify_kernel(int64_t B, int64_t C, int64_t Hh, int64_t Ww, int64_t P, const float* __restrict__ px,
+                                T* __restrict__ out) {
+  const int64_t nph = Hh / P, npw = Ww / P, np = nph * npw;
+  const int64_t total = B * np * C * P;  // one thread per (row, c, kh): P consecutive kw
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t kh = i % P, c = (i / P) % C, rp = i / (P * C);
+    const int64_t b = rp / np, pidx = rp % np, ph = pidx / npw, pw = pidx % npw;
+    const float* src = px + ((b * C + c) * Hh + ph * P + kh) * Ww + pw * P;
+    T* dst = out + rp * (C * P * P) + (c * P + kh) * P;
+    for (int64_t kw = 0; kw < P; ++kw) dst[kw] = from_f32<T>(src[kw]);
+  }
+}
+template <typename T>
+__global__ void vit_tokens_fwd_kernel(int64_t B, int64_t NP, int64_t D, const T* __restrict__ patch,
+                                      const float* __restrict__ cls, const float* __restrict__ pos, T* __restrict__ out) {
+  const int64_t total = B * (NP + 1) * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = i % D, t = (i / D) % (NP + 1), b = i / ((NP + 1) * D);
+    const float base = t == 0 ? cls[d] : to_f32(patch[(b * NP + t - 1) * D + d]);
+    out[i] = from_f32<T>(base + pos[t * D + d]);
+  }
+}
+template <typename T>
+__global__ void vit_tokens_dpatch_kernel(int64_t B, int64_t NP, int64_t D, const T* __restrict__ dout, T* __restrict__ dpatch) {
+  const int64_t total = B * NP * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = i % D, pr = i / D, b = pr / NP, t = pr % NP + 1;
+    dpatch[i] = dout[(b * (NP + 1) + t) * D + d];
+  }
+}
+template <typename T>
+__global__ void vit_tokens_dpos_kernel(int64_t B, int64_t NP, int64_t D, const T* __restrict__ dout, float* __restrict__ dcls,
+                                       float* __restrict__ dpos) {
+  const int64_t n = (NP + 1) * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t b = 0; b < B; ++b) s += to_f32(dout[b * n + i]);
+    dpos[i] = s;
+    if (i < D) dcls[i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// AdamW (torch.optim.AdamW, decoupled weight decay), multi-tensor: grid.y = tensor index
+// ---------------------------------------------------------------------------------------------
+__global__ void step_inc_kernel(const mmfd_adamw_tensor* __restrict__ tab, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) tab[i].step[0] += 1.0f;
+}
+
+__global__ void adamw_kernel(const mmfd_adamw_tensor* __restrict__ tab, float lr, float b1, float b2, float eps, float wd) {
+  const mmfd_adamw_tensor t = tab[blockIdx.y];
+  const double step = (double)t.step[0];
+  const float bc1 = (float)(1.0 - pow((double)b1, step));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, step));
+  const float step_size = lr / bc1;
+  const float decay = 1.0f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.numel; i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = t.grad[i];
+    float p = t.param[i] * decay;
+    float m = t.exp_avg[i];
+    m = m + (1.0f - b1) * (g - m);
+    float v = t.exp_avg_sq[i] * b2 + (1.0f - b2) * g * g;
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p - step_size * (m / denom);
+    t.param[i] = p;
+    t.exp_avg[i] = m;
+    t.exp_avg_sq[i] = v;
+    if (t.param_bf16) reinterpret_cast<bf16*>(t.param_bf16)[i] = (bf16)p;
+  }
+}
+
+__global__ void mask_bias_kernel(int64_t n, const int64_t* __restrict__ mask, float* __restrict__ out, float neg) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = mask[i] ? 0.f : neg;
+}
+}  // namespace
+
+extern "C" int mmfd_seq_mean_fwd(int dtype, int64_t B, int64_t L, int64_t D, const void* x, void* out, int64_t ldo,
+                                 mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(L > 0, "seq_mean: L must be > 0");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((seq_mean_fwd_kernel<bf16>), dim3(gridn(B * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)x, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL((seq_mean_fwd_kernel<float>), dim3(gridn(B * D, 256)), dim3(256), 0, s, B, L, D, (const float*)x, (float*)out, ldo);
+  MMFD_CHECK_LAUNCH("seq_mean_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_seq_mean_bwd(int dtype, int64_t B, int64_t L, int64_t D, const void* dout, int64_t ldo, void* dx,
+                                 mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((seq_mean_bwd_kernel<bf16>), dim3(gridn(B * L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dout, ldo, (bf16*)dx);
+  else
+    hipLaunchKernelGGL((seq_mean_bwd_kernel<float>), dim3(gridn(B * L * D, 256)), dim3(256), 0, s, B, L, D, (const float*)dout, ldo, (float*)dx);
+  MMFD_CHECK_LAUNCH("seq_mean_bwd");
+  return 0;
+}
+
+extern "C" int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits, const int64_t* labels,
+                                 int64_t label_ld, float* loss, float* const* dlogits, const float* dloss_scale,
+                                 mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(n_paths >= 1 && n_paths <= 4, "xent: 1..4 paths");
+  MMFD_CHECK_ARG(B > 0 && C > 0, "xent: bad shape");
+  hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_paths, B, C, logits, labels, label_ld, loss,
+                     dlogits, dloss_scale);
+  MMFD_CHECK_LAUNCH("xent");
+  return 0;
+}
+
+extern "C" int mmfd_embed_ln_fwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                                 const int64_t* token_type_ids, const float* word, const float* pos, const float* type,
+                                 const float* gamma, const float* beta, float eps, void* sum_out, void* y, float* mean,
+                                 float* rstd, float dropout_p, const uint64_t* seed, uint64_t salt, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(D <= 1024, "embed: D <= 1024");
+  MMFD_CHECK_ARG(dropout_p <= 0.f || seed, "embed: dropout needs seed");
+  const int64_t rows = B * L;
+  if (rows == 0) return 0;
+  const float p = dropout_p > 0.f ? dropout_p : 0.f;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, B, L, D, input_ids, token_type_ids, word, pos, type,
+                       gamma, beta, eps, (bf16*)sum_out, (bf16*)y, mean, rstd, p, mmfd_drop_threshold(p), seed, salt);
+  else
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<float>), grid, dim3(256), 0, s, B, L, D, input_ids, token_type_ids, word, pos, type,
+                       gamma, beta, eps, (float*)sum_out, (float*)y, mean, rstd, p, mmfd_drop_threshold(p), seed, salt);
+  MMFD_CHECK_LAUNCH("embed_ln_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                              const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos, float* dtype_emb,
+                              int64_t padding_idx, mmfd_stream_t stream) {
+  const int64_t rows = B * L;
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gw = gridn(rows, 4);
+  const int slabs = (int)std::min<int64_t>(256, std::max<int64_t>(1, rows / 128));
+  dim3 gt((unsigned)((D + 255) / 256), (unsigned)slabs);
+  if (dtype == MMFD_BF16) {
+    if (dword) hipLaunchKernelGGL((embed_word_bwd_kernel<bf16>), dim3(gw), dim3(256), 0, s, rows, D, input_ids, (const bf16*)dsum, dword, padding_idx);
+    if (dpos) hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dsum, dpos);
+    if (dtype_emb) hipLaunchKernelGGL((embed_type_bwd_kernel<bf16>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const bf16*)dsum, dtype_emb);
+  } else {
+    if (dword) hipLaunchKernelGGL((embed_word_bwd_kernel<float>), dim3(gw), dim3(256), 0, s, rows, D, input_ids, (const float*)dsum, dword, padding_idx);
+    if (dpos) hipLaunchKernelGGL((embed_pos_bwd_kernel<float>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const float*)dsum, dpos);
+    if (dtype_emb) hipLaunchKernelGGL((embed_type_bwd_kernel<float>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const float*)dsum, dtype_emb);
+  }
+  MMFD_CHECK_LAUNCH("embed_bwd");
+  return 0;
+}
+
+extern "C" int mmfd_patchify(int dtype, int64_t B, int64_t C, int64_t Hh, int64_t Ww, int64_t P, const float* pixels,
+                             void* out, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(P > 0 && Hh % P == 0 && Ww % P == 0, "patchify: image not divisible by patch");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = B * (Hh / P) * (Ww / P) * C * P;
+  if (total == 0) return 0;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((patchify_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, C, Hh, Ww, P, pixels, (bf16*)out);
+  else
+    hipLaunchKernelGGL((patchify_kernel<float>), dim3(gridn(total, 256)), dim3(256), 0, s, B, C, Hh, Ww, P, pixels, (float*)out);
+  MMFD_CHECK_LAUNCH("patchify");
+  return 0;
+}
+
+extern "C" int mmfd_vit_tokens_fwd(int dtype, int64_t B, int64_t NP, int64_t D, const void* patch, const float* cls,
+                                   const float* pos, void* out, mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = B * (NP + 1) * D;
+  if (total == 0) return 0;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((vit_tokens_fwd_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, NP, D, (const bf16*)patch, cls, pos, (bf16*)out);
+  else
+    hipLaunchKernelGGL((vit_tokens_fwd_kernel<float>), dim3(gridn(total, 256)), dim3(256), 0, s, B, NP, D, (const float*)patch, cls, pos, (float*)out);
+  MMFD_CHECK_LAUNCH("vit_tokens_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_vit_tokens_bwd(int dtype, int64_t B, int64_t NP, int64_t D, const void* dout, void* dpatch, float* dcls,
+                                   float* dpos, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
+  (void)workspace; (void)workspace_bytes;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = B * NP * D;
+  if (dtype == MMFD_BF16) {
+    if (dpatch) hipLaunchKernelGGL((vit_tokens_dpatch_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, NP, D, (const bf16*)dout, (bf16*)dpatch);
+    hipLaunchKernelGGL((vit_tokens_dpos_kernel<bf16>), dim3(gridn((NP + 1) * D, 256)), dim3(256), 0, s, B, NP, D, (const bf16*)dout, dcls, dpos);
+  } else {
+    if (dpatch) hipLaunchKernelGGL((vit_tokens_dpatch_kernel<float>), dim3(gridn(total, 256)), dim3(256), 0, s, B, NP, D, (const float*)dout, (float*)dpatch);
+    hipLaunchKernelGGL((vit_tokens_dpos_kernel<float>), dim3(gridn((NP + 1) * D, 256)), dim3(256), 0, s, B, NP, D, (const float*)dout, dcls, dpos);
+  }
+  MMFD_CHECK_LAUNCH("vit_tokens_bwd");
+  return 0;
+}
+
+extern "C" int mmfd_adamw(int n_tensors, const mmfd_adamw_tensor* table, int64_t max_numel, float lr, float beta1,
+                          float beta2, float eps, float weight_decay, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(n_tensors >= 0 && table, "adamw: bad args");
+  if (n_tensors == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(step_inc_kernel, dim3((unsigned)((n_tensors + 255) / 256)), dim3(256), 0, s, table, n_tensors);
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_numel + 1023) / 1024, 1024));
+  hipLaunchKernelGGL(adamw_kernel, dim3(gx, (unsigned)n_tensors), dim3(256), 0, s, table, lr, beta1, beta2, eps, weight_decay);
+  MMFD_CHECK_LAUNCH("adamw");
+  return 0;
+}
+
+extern "C" int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, float neg, mmfd_stream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mask_bias_kernel, dim3(gridn(n, 256)), dim3(256), 0, (hipStream_t)stream, n, mask, out, neg);
+  MMFD_CHECK_LAUNCH("mask_to_bias");
+  return 0;
+}

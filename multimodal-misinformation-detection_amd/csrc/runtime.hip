@@ -1,0 +1,122 @@
+// Library plumbing (error strings, version, dropout hash) and small elementwise kernels.
+#include "common.h"
+#include <stdarg.h>
+#include <stdio.h>
+#include <algorithm>
+
+static thread_local char g_err[512] = "no error";
+
+int mmfd_set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code == 0 ? MMFD_ERR_INVALID : code;
+}
+
+extern "C" const char* mmfd_last_error_string(void) { return g_err; }
+extern "C" int mmfd_version(void) { return 1; }
+extern "C" uint32_t mmfd_dropout_hash(uint64_t seed, uint64_t salt, uint64_t index) {
+  return mmfd_hash(seed, salt, index);
+}
+
+namespace {
+
+inline int grid_for(int64_t n, int per_block) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, 8192));
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = from_f32<TO>(to_f32(in[i]));
+}
+
+// vectorised fp32 -> bf16 (8 elements per thread-iteration)
+__global__ void cast_f32_bf16_vec(const float4* __restrict__ in, uint4* __restrict__ out, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 a = in[2 * i], b = in[2 * i + 1];
+    bf16x8 v = {(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w, (bf16)b.x, (bf16)b.y, (bf16)b.z, (bf16)b.w};
+    out[i] = __builtin_bit_cast(uint4, v);
+  }
+}
+
+template <typename T>
+__global__ void axpby_kernel(int64_t n, float a, const T* __restrict__ x, float b, const T* __restrict__ y,
+                             T* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = a * to_f32(x[i]);
+    if (y) v += b * to_f32(y[i]);
+    out[i] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void dropout_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ out, float p, uint32_t thr,
+                               const uint64_t* __restrict__ seedp, uint64_t salt) {
+  const uint64_t seed = *seedp;
+  const float sc = 1.0f / (1.0f - p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = mmfd_hash(seed, salt, (uint64_t)i);
+    out[i] = from_f32<T>(h < thr ? 0.0f : to_f32(x[i]) * sc);
+  }
+}
+
+__global__ void seed_advance_kernel(uint64_t* seed) { seed[0] += 1; }
+
+}  // namespace
+
+extern "C" int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  MMFD_CHECK_ARG(in && out, "mmfd_cast: null pointer");
+  if (dtype_in == MMFD_F32 && dtype_out == MMFD_BF16 && (n % 8) == 0 && ((uintptr_t)in & 15) == 0 &&
+      ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(cast_f32_bf16_vec, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const float4*)in, (uint4*)out, n / 8);
+  } else if (dtype_in == MMFD_F32 && dtype_out == MMFD_BF16) {
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, (const float*)in, (bf16*)out, n);
+  } else if (dtype_in == MMFD_BF16 && dtype_out == MMFD_F32) {
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid_for(n, 256)), dim3(256), 0, s, (const bf16*)in, (float*)out, n);
+  } else if (dtype_in == MMFD_F32 && dtype_out == MMFD_F32) {
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n, 256)), dim3(256), 0, s, (const float*)in, (float*)out, n);
+  } else if (dtype_in == MMFD_BF16 && dtype_out == MMFD_BF16) {
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, (const bf16*)in, (bf16*)out, n);
+  } else {
+    return mmfd_set_error(MMFD_ERR_INVALID, "mmfd_cast: bad dtypes %d->%d", dtype_in, dtype_out);
+  }
+  MMFD_CHECK_LAUNCH("cast");
+  return 0;
+}
+
+extern "C" int mmfd_axpby(int dtype, int64_t n, float a, const void* x, float b, const void* y, void* out,
+                          mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((axpby_kernel<bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, (const bf16*)x, b, (const bf16*)y, (bf16*)out);
+  else if (dtype == MMFD_F32)
+    hipLaunchKernelGGL((axpby_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, (const float*)x, b, (const float*)y, (float*)out);
+  else return mmfd_set_error(MMFD_ERR_INVALID, "mmfd_axpby: bad dtype");
+  MMFD_CHECK_LAUNCH("axpby");
+  return 0;
+}
+
+extern "C" int mmfd_dropout(int dtype, int64_t n, const void* x, void* out, float p, const uint64_t* seed,
+                            uint64_t salt, mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MMFD_CHECK_ARG(p >= 0.f && p < 1.f && seed, "mmfd_dropout: bad p/seed");
+  if (n == 0) return 0;
+  const uint32_t thr = mmfd_drop_threshold(p);
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((dropout_kernel<bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const bf16*)x, (bf16*)out, p, thr, seed, salt);
+  else
+    hipLaunchKernelGGL((dropout_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const float*)x, (float*)out, p, thr, seed, salt);
+  MMFD_CHECK_LAUNCH("dropout");
+  return 0;
+}
+
+extern "C" int mmfd_seed_advance(uint64_t* seed, mmfd_stream_t stream) {
+  hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, seed);
+  MMFD_CHECK_LAUNCH("seed_advance");
+  return 0;
+}

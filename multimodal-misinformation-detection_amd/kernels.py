@@ -1,0 +1,520 @@
+"""ctypes binding of libmmfd_hip.so (the C ABI declared in include/mmfd.h) plus thin torch-tensor
+wrappers. PyTorch only provides device memory, the current HIP stream and autograd plumbing; every
+computation below is a launch of one of our gfx950 kernels.
+
+There is no fallback: if the shared library is missing or cannot be loaded, every op raises
+`NativeLibraryError` (the product path must never silently run on something else).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import zlib
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmmfd_hip.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class EpilogueArgs(ctypes.Structure):
+    _fields_ = [
+        ("bias", ctypes.c_void_p),
+        ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int64),
+        ("aux", ctypes.c_void_p), ("ldaux", ctypes.c_int64),
+        ("act", ctypes.c_int),
+        ("dropout_p", ctypes.c_float),
+        ("seed", ctypes.c_void_p),
+        ("salt", ctypes.c_uint64),
+    ]
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int), ("trans_a", ctypes.c_int), ("trans_b", ctypes.c_int),
+        ("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
+        ("A", ctypes.c_void_p), ("lda", ctypes.c_int64),
+        ("B", ctypes.c_void_p), ("ldb", ctypes.c_int64),
+        ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("c_dtype", ctypes.c_int),
+        ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
+        ("ep", EpilogueArgs),
+        ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("splits", ctypes.c_int),
+    ]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int),
+        ("B", ctypes.c_int64), ("H", ctypes.c_int64), ("Lq", ctypes.c_int64), ("Lk", ctypes.c_int64),
+        ("D", ctypes.c_int64),
+        ("scale", ctypes.c_float),
+        ("q", ctypes.c_void_p), ("q_sb", ctypes.c_int64), ("q_st", ctypes.c_int64),
+        ("k", ctypes.c_void_p), ("k_sb", ctypes.c_int64), ("k_st", ctypes.c_int64),
+        ("v", ctypes.c_void_p), ("v_sb", ctypes.c_int64), ("v_st", ctypes.c_int64),
+        ("o", ctypes.c_void_p), ("o_sb", ctypes.c_int64), ("o_st", ctypes.c_int64),
+        ("lse", ctypes.c_void_p),
+        ("key_bias", ctypes.c_void_p),
+        ("rel_bias", ctypes.c_void_p),
+        ("dropout_p", ctypes.c_float), ("seed", ctypes.c_void_p), ("salt", ctypes.c_uint64),
+        ("dout", ctypes.c_void_p), ("do_sb", ctypes.c_int64), ("do_st", ctypes.c_int64),
+        ("dq", ctypes.c_void_p), ("dq_sb", ctypes.c_int64), ("dq_st", ctypes.c_int64),
+        ("dk", ctypes.c_void_p), ("dk_sb", ctypes.c_int64), ("dk_st", ctypes.c_int64),
+        ("dv", ctypes.c_void_p), ("dv_sb", ctypes.c_int64), ("dv_st", ctypes.c_int64),
+        ("delta", ctypes.c_void_p),
+        ("d_rel_bias", ctypes.c_void_p),
+        ("accumulate_dq", ctypes.c_int),
+        ("accumulate_dkv", ctypes.c_int),
+    ]
+
+
+class AdamWTensor(ctypes.Structure):
+    _fields_ = [
+        ("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p), ("param_bf16", ctypes.c_void_p), ("step", ctypes.c_void_p),
+        ("numel", ctypes.c_int64),
+    ]
+
+
+_VP, _I64, _I, _F, _U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
+
+# name -> (restype, argtypes); every symbol declared in include/mmfd.h
+SIGNATURES = {
+    "mmfd_last_error_string": (ctypes.c_char_p, []),
+    "mmfd_version": (_I, []),
+    "mmfd_dropout_hash": (ctypes.c_uint32, [_U64, _U64, _U64]),
+    "mmfd_gemm": (_I, [ctypes.POINTER(GemmArgs), _VP]),
+    "mmfd_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmArgs)]),
+    "mmfd_colsum": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _F, _VP, _I64, _VP]),
+    "mmfd_attn_fwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
+    "mmfd_attn_bwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
+    "mmfd_layernorm_fwd": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP]),
+    "mmfd_layernorm_bwd": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _I64, _VP, _I64,
+                                _VP, _VP, _F, _VP, _F, _VP, _U64, _VP, _I64, _VP]),
+    "mmfd_seq_mean_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _I64, _VP]),
+    "mmfd_seq_mean_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _I64, _VP, _VP]),
+    "mmfd_xent_fwd_bwd": (_I, [_I, _I64, _I64, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
+    "mmfd_embed_ln_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
+                               _F, _VP, _U64, _VP]),
+    "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    "mmfd_mask_to_bias": (_I, [_I64, _VP, _VP, _F, _VP]),
+    "mmfd_patchify": (_I, [_I, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _VP]),
+    "mmfd_vit_tokens_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+    "mmfd_vit_tokens_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    "mmfd_adamw": (_I, [_I, _VP, _I64, _F, _F, _F, _F, _F, _VP]),
+    "mmfd_cast": (_I, [_I, _I, _I64, _VP, _VP, _VP]),
+    "mmfd_axpby": (_I, [_I, _I64, _F, _VP, _F, _VP, _VP, _VP]),
+    "mmfd_dropout": (_I, [_I, _I64, _VP, _VP, _F, _VP, _U64, _VP]),
+    "mmfd_seed_advance": (_I, [_VP, _VP]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libmmfd_hip.so (after torch, so the HIP runtime torch already loaded is reused)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeLibraryError(f"{path} not found: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().mmfd_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {dt} (fp32 / bf16)")
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("mmfd kernels need tensors on the GPU (HIP device)")
+
+
+def salt_of(name: str) -> int:
+    """Stable 64-bit call-site id for counter-based dropout."""
+    b = name.encode()
+    return (zlib.crc32(b) << 32) | zlib.crc32(b[::-1] + b"mmfd")
+
+
+# ------------------------------------------------------------------------------------------------
+# step seed (device resident so that captured graphs see it advance)
+# ------------------------------------------------------------------------------------------------
+class Seed:
+    def __init__(self, value: int = 0, device=None):
+        self.t = torch.tensor([value], dtype=torch.int64, device=device or "cuda")
+
+    def ptr(self):
+        return _ptr(self.t)
+
+    def advance(self):
+        _check(lib().mmfd_seed_advance(self.ptr(), _stream()), "seed_advance")
+
+    def set(self, value: int):
+        self.t.fill_(value)
+
+
+# ------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"operand must be a 2-D row-major view, got shape {tuple(t.shape)} strides {t.stride()}")
+    return t.stride(0)
+
+
+def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
+         residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0):
+    """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
+    nn.Linear weight) when trans_b=False, else B ([K,N] stored)."""
+    _require_cuda(A, B, out, bias, residual, aux)
+    if A.dtype != B.dtype:
+        raise TypeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
+    if trans_a:
+        K, M = A.shape
+    else:
+        M, K = A.shape
+    if trans_b:
+        K2, N = B.shape
+    else:
+        N, K2 = B.shape
+    if K != K2:
+        raise ValueError(f"gemm inner dims differ: {K} vs {K2}")
+    if out is None:
+        out = torch.empty((M, N), device=A.device, dtype=out_dtype or A.dtype)
+    if tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm out shape {tuple(out.shape)} != {(M, N)}")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous fp32 vector of length N")
+    for t in (residual, aux):
+        if t is not None and (t.dtype != out.dtype or tuple(t.shape) != (M, N)):
+            raise ValueError("residual/aux must match the output shape and dtype")
+    if dropout_p > 0 and seed is None:
+        raise ValueError("dropout needs a Seed")
+    a = GemmArgs()
+    a.dtype = dtype_code(A.dtype)
+    a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
+    a.M, a.N, a.K = M, N, K
+    a.A, a.lda = A.data_ptr(), _ld(A)
+    a.B, a.ldb = B.data_ptr(), _ld(B)
+    a.C, a.ldc, a.c_dtype = out.data_ptr(), _ld(out), dtype_code(out.dtype)
+    a.alpha, a.beta = float(alpha), float(beta)
+    a.ep.bias = bias.data_ptr() if bias is not None else None
+    if residual is not None:
+        a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
+    if aux is not None:
+        a.ep.aux, a.ep.ldaux = aux.data_ptr(), _ld(aux)
+    a.ep.act = int(act)
+    a.ep.dropout_p = float(dropout_p)
+    a.ep.seed = seed.t.data_ptr() if seed is not None else None
+    a.ep.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    a.splits = int(splits)
+    L = lib()
+    need = L.mmfd_gemm_workspace_bytes(ctypes.byref(a))
+    ws = None
+    if need > 0:
+        ws = torch.empty(need // 4 + 1, device=A.device, dtype=torch.float32)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), need
+    _check(L.mmfd_gemm(ctypes.byref(a), _stream()), "mmfd_gemm")
+    return out
+
+
+def colsum(X, out=None, beta=0.0):
+    _require_cuda(X)
+    M, N = X.shape
+    if out is None:
+        out = torch.empty(N, device=X.device, dtype=torch.float32)
+    nparts = max(1, min(256, M // 64))
+    ws = torch.empty(nparts * N, device=X.device, dtype=torch.float32)
+    _check(lib().mmfd_colsum(dtype_code(X.dtype), M, N, _ptr(X), _ld(X), _ptr(out), float(beta), _ptr(ws),
+                             ws.numel() * 4, _stream()), "mmfd_colsum")
+    return out
+
+
+def linear(x, w, b=None, **kw):
+    """y = x @ w^T + b over the last dim (x: [..., K], w: [N, K])."""
+    shp = x.shape
+    y = gemm(x.reshape(-1, shp[-1]), w, bias=b, **kw)
+    return y.reshape(*shp[:-1], w.shape[0])
+
+
+# ------------------------------------------------------------------------------------------------
+# attention
+# ------------------------------------------------------------------------------------------------
+def _head_view(t, H, D):
+    """t: [B, L, >= H*D] view with unit stride on the last dim -> (ptr, s_b, s_t)."""
+    if t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError("attention operands must be [B, L, H*D] views with a contiguous last dim")
+    return t.data_ptr(), t.stride(0), t.stride(1)
+
+
+def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, dropout_p=0.0, seed=None, salt=0):
+    """q: [B, Lq, H*D], k/v: [B, Lk, H*D] (views into fused QKV buffers are fine).
+    Returns (o [B, Lq, H*D], lse [B, H, Lq] fp32)."""
+    _require_cuda(q, k, v)
+    B, Lq, HD = q.shape
+    Lk = k.shape[1]
+    D = HD // H
+    if out is None:
+        out = torch.empty((B, Lq, H * D), device=q.device, dtype=q.dtype)
+    lse = torch.empty((B, H, Lq), device=q.device, dtype=torch.float32)
+    a = AttnArgs()
+    a.dtype = dtype_code(q.dtype)
+    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
+    a.scale = float(scale if scale is not None else D ** -0.5)
+    a.q, a.q_sb, a.q_st = _head_view(q, H, D)
+    a.k, a.k_sb, a.k_st = _head_view(k, H, D)
+    a.v, a.v_sb, a.v_st = _head_view(v, H, D)
+    a.o, a.o_sb, a.o_st = _head_view(out, H, D)
+    a.lse = lse.data_ptr()
+    a.key_bias = key_bias.data_ptr() if key_bias is not None else None
+    a.rel_bias = rel_bias.data_ptr() if rel_bias is not None else None
+    a.dropout_p = float(dropout_p)
+    a.seed = seed.t.data_ptr() if seed is not None else None
+    a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    _check(lib().mmfd_attn_fwd(ctypes.byref(a), _stream()), "mmfd_attn_fwd")
+    return out, lse
+
+
+def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None, key_bias=None, rel_bias=None,
+             dropout_p=0.0, seed=None, salt=0, accumulate_dq=False, accumulate_dkv=False):
+    _require_cuda(q, k, v, o, lse, dout)
+    B, Lq, HD = q.shape
+    Lk = k.shape[1]
+    D = HD // H
+    dq = dq if dq is not None else torch.empty_like(q, memory_format=torch.contiguous_format)
+    dk = dk if dk is not None else torch.empty((B, Lk, HD), device=q.device, dtype=q.dtype)
+    dv = dv if dv is not None else torch.empty((B, Lk, HD), device=q.device, dtype=q.dtype)
+    delta = torch.empty((B, H, Lq), device=q.device, dtype=torch.float32)
+    a = AttnArgs()
+    a.dtype = dtype_code(q.dtype)
+    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
+    a.scale = float(scale if scale is not None else D ** -0.5)
+    a.q, a.q_sb, a.q_st = _head_view(q, H, D)
+    a.k, a.k_sb, a.k_st = _head_view(k, H, D)
+    a.v, a.v_sb, a.v_st = _head_view(v, H, D)
+    a.o, a.o_sb, a.o_st = _head_view(o, H, D)
+    a.lse = lse.data_ptr()
+    a.key_bias = key_bias.data_ptr() if key_bias is not None else None
+    a.rel_bias = rel_bias.data_ptr() if rel_bias is not None else None
+    a.dropout_p = float(dropout_p)
+    a.seed = seed.t.data_ptr() if seed is not None else None
+    a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    a.dout, a.do_sb, a.do_st = _head_view(dout, H, D)
+    a.dq, a.dq_sb, a.dq_st = _head_view(dq, H, D)
+    a.dk, a.dk_sb, a.dk_st = _head_view(dk, H, D)
+    a.dv, a.dv_sb, a.dv_st = _head_view(dv, H, D)
+    a.delta = delta.data_ptr()
+    a.accumulate_dq, a.accumulate_dkv = int(accumulate_dq), int(accumulate_dkv)
+    _check(lib().mmfd_attn_bwd(ctypes.byref(a), _stream()), "mmfd_attn_bwd")
+    return dq, dk, dv
+
+
+# ------------------------------------------------------------------------------------------------
+# LayerNorm
+# ------------------------------------------------------------------------------------------------
+def layernorm_fwd(x2d, gamma, beta, eps, out=None):
+    _require_cuda(x2d, gamma, beta)
+    R, W = x2d.shape
+    y = out if out is not None else torch.empty((R, W), device=x2d.device, dtype=x2d.dtype)
+    mean = torch.empty(R, device=x2d.device, dtype=torch.float32)
+    rstd = torch.empty(R, device=x2d.device, dtype=torch.float32)
+    _check(lib().mmfd_layernorm_fwd(dtype_code(x2d.dtype), R, W, _ptr(x2d), _ld(x2d), _ptr(gamma), _ptr(beta),
+                                    float(eps), _ptr(y), _ld(y), _ptr(mean), _ptr(rstd), _stream()),
+           "mmfd_layernorm_fwd")
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None, dbeta=None, beta_acc=0.0,
+                  dx_drop=None, dropout_p=0.0, seed=None, salt=0):
+    _require_cuda(dy, x, gamma, mean, rstd)
+    R, W = dy.shape
+    dx = dx if dx is not None else torch.empty((R, W), device=dy.device, dtype=dy.dtype)
+    nb = max(1, min((R + 3) // 4, 512))
+    ws = torch.empty(nb * 2 * W, device=dy.device, dtype=torch.float32)
+    _check(lib().mmfd_layernorm_bwd(dtype_code(dy.dtype), R, W, _ptr(dy), _ld(dy), _ptr(x), _ld(x), _ptr(gamma),
+                                    _ptr(mean), _ptr(rstd), _ptr(dx), _ld(dx), _ptr(dx_add),
+                                    _ld(dx_add) if dx_add is not None else 0, _ptr(dgamma), _ptr(dbeta),
+                                    float(beta_acc), _ptr(dx_drop), float(dropout_p),
+                                    seed.ptr() if seed is not None else None, int(salt) & 0xFFFFFFFFFFFFFFFF,
+                                    _ptr(ws), ws.numel() * 4, _stream()), "mmfd_layernorm_bwd")
+    return dx
+
+
+# ------------------------------------------------------------------------------------------------
+# misc
+# ------------------------------------------------------------------------------------------------
+def seq_mean_fwd(x, out=None):
+    B, L, D = x.shape
+    out = out if out is not None else torch.empty((B, D), device=x.device, dtype=x.dtype)
+    _check(lib().mmfd_seq_mean_fwd(dtype_code(x.dtype), B, L, D, _ptr(x.contiguous()), _ptr(out), _ld(out),
+                                   _stream()), "mmfd_seq_mean_fwd")
+    return out
+
+
+def seq_mean_bwd(dout, L, dx=None):
+    B, D = dout.shape
+    dx = dx if dx is not None else torch.empty((B, L, D), device=dout.device, dtype=dout.dtype)
+    _check(lib().mmfd_seq_mean_bwd(dtype_code(dout.dtype), B, L, D, _ptr(dout), _ld(dout), _ptr(dx), _stream()),
+           "mmfd_seq_mean_bwd")
+    return dx
+
+
+class _PtrArray:
+    """A small device array of device pointers (kept alive with its tensors)."""
+
+    def __init__(self, tensors, device):
+        self.tensors = list(tensors)
+        host = torch.tensor([t.data_ptr() for t in self.tensors], dtype=torch.int64)
+        self.dev = host.to(device, non_blocking=False)
+
+    def ptr(self):
+        return _ptr(self.dev)
+
+
+def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None):
+    """logits: list of [B, C] fp32 tensors (paths), labels: int64 [B, n_paths (or more)].
+    Returns (loss [1 + n_paths] fp32 device tensor, list of dlogits or None)."""
+    n = len(logits)
+    B, C = logits[0].shape
+    dev = logits[0].device
+    logits = [l.contiguous().float() for l in logits]
+    labels = labels.contiguous()
+    loss = torch.empty(1 + n, device=dev, dtype=torch.float32)
+    lp = _PtrArray(logits, dev)
+    dl = [torch.empty_like(l) for l in logits] if want_grad else None
+    dp = _PtrArray(dl, dev) if want_grad else None
+    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp.ptr(), _ptr(labels), labels.stride(0), _ptr(loss),
+                                   dp.ptr() if dp is not None else None, _ptr(dloss_scale), _stream()),
+           "mmfd_xent_fwd_bwd")
+    return loss, dl
+
+
+def cast(x, dtype):
+    out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    if x.numel():
+        _check(lib().mmfd_cast(dtype_code(x.dtype), dtype_code(dtype), x.numel(), _ptr(x.contiguous()), _ptr(out),
+                               _stream()), "mmfd_cast")
+    return out
+
+
+def axpby(a, x, b=0.0, y=None, out=None):
+    out = out if out is not None else torch.empty_like(x)
+    _check(lib().mmfd_axpby(dtype_code(x.dtype), x.numel(), float(a), _ptr(x), float(b), _ptr(y), _ptr(out),
+                            _stream()), "mmfd_axpby")
+    return out
+
+
+def dropout(x, p, seed, salt, out=None):
+    out = out if out is not None else torch.empty_like(x)
+    _check(lib().mmfd_dropout(dtype_code(x.dtype), x.numel(), _ptr(x), _ptr(out), float(p), seed.ptr(),
+                              int(salt) & 0xFFFFFFFFFFFFFFFF, _stream()), "mmfd_dropout")
+    return out
+
+
+def mask_to_bias(mask, neg=None):
+    neg = torch.finfo(torch.float32).min if neg is None else neg
+    m = mask.to(torch.int64).contiguous()
+    out = torch.empty(m.shape, device=m.device, dtype=torch.float32)
+    _check(lib().mmfd_mask_to_bias(m.numel(), _ptr(m), _ptr(out), float(neg), _stream()), "mmfd_mask_to_bias")
+    return out
+
+
+def embed_ln_fwd(ids, tts, word, pos, typ, gamma, beta, eps, dtype, dropout_p=0.0, seed=None, salt=0):
+    B, L = ids.shape
+    D = word.shape[1]
+    dev = ids.device
+    s = torch.empty((B * L, D), device=dev, dtype=dtype)
+    y = torch.empty((B * L, D), device=dev, dtype=dtype)
+    mean = torch.empty(B * L, device=dev, dtype=torch.float32)
+    rstd = torch.empty(B * L, device=dev, dtype=torch.float32)
+    _check(lib().mmfd_embed_ln_fwd(dtype_code(dtype), B, L, D, _ptr(ids.contiguous()),
+                                   _ptr(tts.contiguous()) if tts is not None else None, _ptr(word), _ptr(pos),
+                                   _ptr(typ), _ptr(gamma), _ptr(beta), float(eps), _ptr(s), _ptr(y), _ptr(mean),
+                                   _ptr(rstd), float(dropout_p), seed.ptr() if seed is not None else None,
+                                   int(salt) & 0xFFFFFFFFFFFFFFFF, _stream()), "mmfd_embed_ln_fwd")
+    return s, y, mean, rstd
+
+
+def embed_bwd(ids, tts, dsum, dword, dpos, dtype_emb, padding_idx=-1):
+    B, L = ids.shape
+    D = dsum.shape[-1]
+    _check(lib().mmfd_embed_bwd(dtype_code(dsum.dtype), B, L, D, _ptr(ids), _ptr(tts) if tts is not None else None,
+                                _ptr(dsum), _ptr(dword), _ptr(dpos), _ptr(dtype_emb), int(padding_idx), _stream()),
+           "mmfd_embed_bwd")
+
+
+def patchify(pixels, P, dtype):
+    B, C, Hh, Ww = pixels.shape
+    npch = (Hh // P) * (Ww // P)
+    out = torch.empty((B * npch, C * P * P), device=pixels.device, dtype=dtype)
+    _check(lib().mmfd_patchify(dtype_code(dtype), B, C, Hh, Ww, P, _ptr(pixels.contiguous().float()), _ptr(out),
+                               _stream()), "mmfd_patchify")
+    return out
+
+
+def vit_tokens_fwd(patch, B, cls, pos):
+    NP = patch.shape[0] // B
+    D = patch.shape[1]
+    out = torch.empty((B, NP + 1, D), device=patch.device, dtype=patch.dtype)
+    _check(lib().mmfd_vit_tokens_fwd(dtype_code(patch.dtype), B, NP, D, _ptr(patch), _ptr(cls), _ptr(pos), _ptr(out),
+                                     _stream()), "mmfd_vit_tokens_fwd")
+    return out
+
+
+def vit_tokens_bwd(dout, want_dpatch=True):
+    B, T, D = dout.shape
+    NP = T - 1
+    dpatch = torch.empty((B * NP, D), device=dout.device, dtype=dout.dtype) if want_dpatch else None
+    dcls = torch.empty(D, device=dout.device, dtype=torch.float32)
+    dpos = torch.empty((T, D), device=dout.device, dtype=torch.float32)
+    _check(lib().mmfd_vit_tokens_bwd(dtype_code(dout.dtype), B, NP, D, _ptr(dout.contiguous()), _ptr(dpatch),
+                                     _ptr(dcls), _ptr(dpos), None, 0, _stream()), "mmfd_vit_tokens_bwd")
+    return dpatch, dcls, dpos
+
+
+def adamw(table_dev, n, max_numel, lr, beta1, beta2, eps, weight_decay):
+    _check(lib().mmfd_adamw(int(n), _ptr(table_dev), int(max_numel), float(lr), float(beta1), float(beta2),
+                            float(eps), float(weight_decay), _stream()), "mmfd_adamw")
+
+
+def dropout_hash(seed: int, salt: int, index: int) -> int:
+    return int(lib().mmfd_dropout_hash(seed & 0xFFFFFFFFFFFFFFFF, salt & 0xFFFFFFFFFFFFFFFF, index))

@@ -1,0 +1,68 @@
+"""Drop-in for `torch.optim.AdamW` (train.py:8, 356, 188) backed by one multi-tensor HIP launch.
+
+Same math as torch's AdamW (decoupled weight decay, bias correction with a per-parameter step),
+same state keys ('step', 'exp_avg', 'exp_avg_sq'); parameters whose .grad is None are skipped,
+exactly like torch (the reference's `text_self_ln2` / `image_self_ln2` never receive gradients).
+The pointer table is cached, so a step can be captured in a hipGraph once warmed up.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import kernels as K
+
+
+class AdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
+            raise ValueError("invalid AdamW hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._tables = {}
+
+    def _table(self, entries, device):
+        key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s.data_ptr(), p.numel())
+                    for p, g, m, v, s in entries)
+        t = self._tables.get(key)
+        if t is None:
+            arr = (K.AdamWTensor * len(entries))()
+            for i, (p, g, m, v, s) in enumerate(entries):
+                arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
+                arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
+                arr[i].param_bf16 = None
+                arr[i].step = s.data_ptr()
+                arr[i].numel = p.numel()
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            t = host.to(device)
+            self._tables[key] = t
+        return t
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            entries = []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                    raise TypeError("mmfd AdamW keeps fp32 master parameters and gradients")
+                if not (p.is_contiguous() and p.grad.is_contiguous()):
+                    raise ValueError("mmfd AdamW needs contiguous params/grads")
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                entries.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step"]))
+            if not entries:
+                continue
+            b1, b2 = group["betas"]
+            table = self._table(entries, entries[0][0].device)
+            K.adamw(table, len(entries), max(e[0].numel() for e in entries), group["lr"], b1, b2, group["eps"],
+                    group["weight_decay"])
+        return loss

@@ -1,0 +1,53 @@
+"""TEST INFRASTRUCTURE ONLY (oracle). Never imported by the product path.
+
+numpy restatement of the counter-based dropout hash used by every mmfd kernel
+(multimodal-misinformation-detection_amd/csrc/common.h: mmfd_mix32 / mmfd_hash /
+mmfd_drop_threshold). The reference draws dropout masks from torch's RNG (layers.py:15,17,53;
+model.py:255-288); torch's CPU and GPU streams differ anyway, so parity in train mode is checked
+against THIS mask: the oracle applies the same mask to the reference math.
+"""
+import numpy as np
+
+_M1 = np.uint32(0x7FEB352D)
+_M2 = np.uint32(0x846CA68B)
+
+
+def mix32(x):
+    x = np.asarray(x, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint32(16))
+        x = (x * _M1).astype(np.uint32)
+        x = x ^ (x >> np.uint32(15))
+        x = (x * _M2).astype(np.uint32)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
+def dropout_hash(seed: int, salt: int, idx):
+    idx = np.asarray(idx, dtype=np.uint64)
+    lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    hi = (idx >> np.uint64(32)).astype(np.uint32)
+    salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    with np.errstate(over="ignore"):
+        h = mix32(lo)
+        h = mix32(h ^ hi ^ np.uint32(0x9E3779B9))
+        s_hi = np.uint32(((salt >> 32) * 0x85EBCA6B) & 0xFFFFFFFF)
+        h = mix32(h ^ np.uint32(salt & 0xFFFFFFFF) ^ s_hi)
+        h = mix32(h ^ np.uint32(seed & 0xFFFFFFFF))
+        h = mix32(h ^ np.uint32(seed >> 32))
+    return h
+
+
+def drop_threshold(p: float) -> int:
+    t = float(np.float32(p)) * 4294967296.0
+    if t >= 4294967295.0:
+        return 0xFFFFFFFF
+    return int(t)
+
+
+def keep_mask(seed: int, salt: int, shape, p: float):
+    """Boolean keep-mask for a contiguous tensor of `shape` (element index = flat index)."""
+    n = int(np.prod(shape))
+    h = dropout_hash(seed, salt, np.arange(n, dtype=np.uint64))
+    return (h >= np.uint32(drop_threshold(p))).reshape(shape)

@@ -1,0 +1,264 @@
+"""Kernel-level numerics of libmmfd_hip.so against plain PyTorch fp64/fp32 references (CPU).
+
+Tolerances: fp32 kernels accumulate in fp32 on MFMA (exact fp32 products) -> rel 2e-5 of the
+operand scale; bf16 kernels round inputs/outputs to bf16 (8 significant bits) -> rel 2e-2.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import mmfd
+from mmfd import kernels as K
+from oracle.dropout_hash import keep_mask
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tol(dtype):
+    return (3e-5, 3e-5) if dtype == torch.float32 else (2e-2, 2e-2)
+
+
+def _close(got, ref, dtype, scale=1.0):
+    rtol, atol = _tol(dtype)
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    err = (got - ref).abs().max().item()
+    bound = atol * scale + rtol * ref.abs().max().item()
+    assert err <= bound, f"max err {err:.3e} > {bound:.3e}"
+
+
+def _rand(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# GEMM
+# ---------------------------------------------------------------------------------------------
+SHAPES = [(128, 128, 64), (256, 384, 768), (200, 136, 96), (37, 24, 40), (1000, 256, 512), (64, 3072, 768)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_gemm_layouts(dtype, layout, shape):
+    M, N, Kd = shape
+    if layout == "nt":  # y = x W^T
+        A = _rand(M, Kd, dtype=dtype, seed=1); B = _rand(N, Kd, dtype=dtype, seed=2)
+        ref = A.double() @ B.double().T
+        out = K.gemm(A.to(DEV), B.to(DEV), out_dtype=torch.float32)
+    elif layout == "nn":  # dX = dY W
+        A = _rand(M, Kd, dtype=dtype, seed=1); B = _rand(Kd, N, dtype=dtype, seed=2)
+        ref = A.double() @ B.double()
+        out = K.gemm(A.to(DEV), B.to(DEV), trans_b=True, out_dtype=torch.float32)
+    else:  # dW = dY^T X
+        A = _rand(Kd, M, dtype=dtype, seed=1); B = _rand(Kd, N, dtype=dtype, seed=2)
+        ref = A.double().T @ B.double()
+        out = K.gemm(A.to(DEV), B.to(DEV), trans_a=True, trans_b=True, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    rtol = 2e-5 if dtype == torch.float32 else 2e-5  # inputs exact in both; fp32 accumulation
+    err = (out.double().cpu() - ref).abs().max().item()
+    assert err <= rtol * math.sqrt(Kd) * 4 + 1e-4, err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_long_k(dtype):
+    # dW of a BERT-like layer: K (tokens) long, small output -> split-K path
+    Kd, M, N = 8192, 256, 384
+    A = _rand(Kd, M, dtype=dtype, seed=3); B = _rand(Kd, N, dtype=dtype, seed=4)
+    ref = A.double().T @ B.double()
+    out = K.gemm(A.to(DEV), B.to(DEV), trans_a=True, trans_b=True, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    err = (out.double().cpu() - ref).abs().max().item()
+    assert err <= 2e-3 * math.sqrt(Kd / 1024), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    M, N, Kd = 300, 256, 128
+    x = _rand(M, Kd, dtype=dtype, seed=5); w = _rand(N, Kd, dtype=dtype, seed=6, scale=0.1)
+    b = _rand(N, seed=7)
+    res = _rand(M, N, dtype=dtype, seed=8)
+    base = x.double() @ w.double().T + b.double()
+    # gelu + aux
+    aux = torch.empty(M, N, device=DEV, dtype=dtype)
+    y = K.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=K.ACT_GELU, aux=aux)
+    torch.cuda.synchronize()
+    _close(aux, base, dtype, 1.0)
+    _close(y, torch.nn.functional.gelu(base), dtype, 1.0)
+    # relu + residual
+    y = K.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=K.ACT_RELU, residual=res.to(DEV))
+    _close(y, base.clamp_min(0) + res.double(), dtype, 1.0)
+    # beta accumulate
+    c0 = res.to(DEV).clone()
+    K.gemm(x.to(DEV), w.to(DEV), out=c0, beta=1.0)
+    _close(c0, x.double() @ w.double().T + res.double(), dtype, 1.0)
+    # gelu backward
+    pre = base.to(dtype)
+    gy = K.gemm(x.to(DEV), w.to(DEV), act=K.ACT_GELU_BWD, aux=pre.to(DEV))
+    t = pre.double().requires_grad_(True)
+    torch.nn.functional.gelu(t).backward(torch.ones_like(t))
+    _close(gy, (x.double() @ w.double().T) * t.grad, dtype, 1.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_dropout_mask(dtype):
+    M, N, Kd = 256, 128, 64
+    x = _rand(M, Kd, dtype=dtype, seed=9); w = _rand(N, Kd, dtype=dtype, seed=10)
+    seed = K.Seed(1234)
+    salt = K.salt_of("test.gemm.dropout")
+    y = K.gemm(x.to(DEV), w.to(DEV), dropout_p=0.1, seed=seed, salt=salt, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(keep_mask(1234, salt, (M, N), 0.1))
+    ref = (x.double() @ w.double().T) * keep / 0.9
+    _close(y, ref, torch.float32 if dtype == torch.float32 else torch.bfloat16)
+    frac = keep.float().mean().item()
+    assert 0.88 < frac < 0.92
+
+
+def test_dropout_hash_host_matches_numpy():
+    from oracle.dropout_hash import dropout_hash
+    for seed, salt, idx in [(0, 0, 0), (1234, K.salt_of("x"), 17), (2**40 + 5, 2**63 + 11, 2**35 + 3)]:
+        assert K.dropout_hash(seed, salt, idx) == int(dropout_hash(seed, salt, np.array([idx], dtype=np.uint64))[0])
+
+
+def test_colsum():
+    for dtype in (torch.float32, torch.bfloat16):
+        X = _rand(5000, 300, dtype=dtype, seed=11)
+        got = K.colsum(X.to(DEV))
+        torch.cuda.synchronize()
+        ref = X.double().sum(0)
+        assert (got.double().cpu() - ref).abs().max().item() < 1e-2
+
+
+# ---------------------------------------------------------------------------------------------
+# attention
+# ---------------------------------------------------------------------------------------------
+def _attn_ref(q, k, v, H, scale, key_bias=None, keep=None, p=0.0):
+    B, Lq, HD = q.shape
+    D = HD // H
+    qh = q.double().view(B, Lq, H, D).transpose(1, 2)
+    kh = k.double().view(B, -1, H, D).transpose(1, 2)
+    vh = v.double().view(B, -1, H, D).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale
+    if key_bias is not None:
+        s = s + key_bias.double()[:, None, None, :]
+    pr = torch.softmax(s, -1)
+    lse = torch.logsumexp(s, -1)
+    pd = pr * keep / (1 - p) if keep is not None else pr
+    o = (pd @ vh).transpose(1, 2).reshape(B, Lq, HD)
+    return o, lse
+
+
+ATTN_CASES = [(2, 4, 128, 128, 64), (2, 8, 197, 197, 32), (3, 2, 13, 29, 64), (2, 8, 128, 197, 32),
+              (1, 12, 70, 70, 64)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ATTN_CASES)
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_bwd(dtype, case, masked, p):
+    B, H, Lq, Lk, D = case
+    q = _rand(B, Lq, H * D, dtype=dtype, seed=20)
+    kv = _rand(B, Lk, 2 * H * D, dtype=dtype, seed=21)  # fused K|V buffer -> strided views
+    k, v = kv[..., : H * D], kv[..., H * D:]
+    dout = _rand(B, Lq, H * D, dtype=dtype, seed=22)
+    scale = D ** -0.5
+    kb = None
+    if masked:
+        lens = torch.randint(1, Lk + 1, (B,), generator=torch.Generator().manual_seed(3))
+        mask = (torch.arange(Lk)[None, :] < lens[:, None]).long()
+        kb = K.mask_to_bias(mask.to(DEV))
+        kb_cpu = kb.cpu()
+    else:
+        kb_cpu = None
+    seed = K.Seed(77)
+    salt = K.salt_of("test.attn")
+    keep = None
+    if p > 0:
+        keep = torch.from_numpy(keep_mask(77, salt, (B, H, Lq, Lk), p)).double()
+    qd, kvd, dod = q.to(DEV), kv.to(DEV), dout.to(DEV)
+    o, lse = K.attn_fwd(qd, kvd[..., : H * D], kvd[..., H * D:], H, key_bias=kb, dropout_p=p, seed=seed, salt=salt)
+    dq, dk, dv = K.attn_bwd(qd, kvd[..., : H * D], kvd[..., H * D:], o, lse, dod, H, key_bias=kb, dropout_p=p,
+                            seed=seed, salt=salt)
+    torch.cuda.synchronize()
+    # reference on the kernel's (rounded) inputs
+    qr = q.double().requires_grad_(True)
+    kr = k.double().requires_grad_(True)
+    vr = v.double().requires_grad_(True)
+    oref, lref = _attn_ref(qr, kr, vr, H, scale, kb_cpu, keep, p)
+    oref.backward(dout.double())
+    _close(o, oref, dtype)
+    assert (lse.double().cpu() - lref).abs().max().item() < (1e-4 if dtype == torch.float32 else 2e-2)
+    _close(dq, qr.grad, dtype)
+    _close(dk, kr.grad, dtype)
+    _close(dv, vr.grad, dtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# LayerNorm / misc
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("width,eps", [(256, 1e-5), (768, 1e-12), (384, 1e-5)])
+def test_layernorm(dtype, width, eps):
+    R = 1000
+    x = _rand(R, width, dtype=dtype, seed=30, scale=2.0) + 0.5
+    g = _rand(width, seed=31) * 0.1 + 1.0
+    b = _rand(width, seed=32) * 0.1
+    dy = _rand(R, width, dtype=dtype, seed=33)
+    add = _rand(R, width, dtype=dtype, seed=34)
+    y, mean, rstd = K.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV), eps)
+    dg = torch.empty(width, device=DEV); db = torch.empty(width, device=DEV)
+    dx = K.layernorm_bwd(dy.to(DEV), x.to(DEV), g.to(DEV), mean, rstd, dx_add=add.to(DEV), dgamma=dg, dbeta=db)
+    torch.cuda.synchronize()
+    xr = x.double().requires_grad_(True)
+    gr = g.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (width,), gr, br, eps)
+    yr.backward(dy.double())
+    _close(y, yr, dtype, 1.0)
+    _close(dx, xr.grad + add.double(), dtype, 1.0)
+    assert (dg.double().cpu() - gr.grad).abs().max().item() < 1e-3 * R ** 0.5
+    assert (db.double().cpu() - br.grad).abs().max().item() < 1e-3 * R ** 0.5
+
+
+def test_seq_mean_xent():
+    x = _rand(4, 13, 256, seed=40)
+    m = K.seq_mean_fwd(x.to(DEV))
+    dx = K.seq_mean_bwd(torch.ones(4, 256, device=DEV), 13)
+    torch.cuda.synchronize()
+    assert torch.allclose(m.cpu(), x.mean(1), atol=1e-6)
+    assert torch.allclose(dx.cpu(), torch.full((4, 13, 256), 1 / 13), atol=1e-7)
+    logits = [_rand(8, 3, seed=50 + i) for i in range(4)]
+    labels = torch.randint(0, 3, (8, 4), generator=torch.Generator().manual_seed(0))
+    loss, dl = K.xent_fwd_bwd([l.to(DEV) for l in logits], labels.to(DEV))
+    torch.cuda.synchronize()
+    lr = [l.double().requires_grad_(True) for l in logits]
+    tot = sum(torch.nn.functional.cross_entropy(lr[i], labels[:, i]) for i in range(4))
+    tot.backward()
+    assert abs(loss[0].item() - tot.item()) < 1e-5
+    for i in range(4):
+        assert torch.allclose(dl[i].double().cpu(), lr[i].grad, atol=1e-6)
+
+
+def test_adamw_matches_torch():
+    ps = [_rand(1000, seed=60), _rand(37, 5, seed=61)]
+    gs = [_rand(1000, seed=62), _rand(37, 5, seed=63)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    from mmfd.optim import AdamW
+    dev = [p.clone().to(DEV).requires_grad_(True) for p in ps]
+    myopt = AdamW(dev, lr=1e-3, weight_decay=0.01)
+    for it in range(3):
+        for r, d, g in zip(ref, dev, gs):
+            r.grad = g * (it + 1)
+            d.grad = (g * (it + 1)).to(DEV)
+        opt.step()
+        myopt.step()
+    torch.cuda.synchronize()
+    for r, d in zip(ref, dev):
+        assert (r.detach() - d.detach().cpu()).abs().max().item() < 1e-6
