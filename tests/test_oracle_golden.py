@@ -1,0 +1,134 @@
+"""Pins the CPU oracle (oracle/) against fixtures produced by the reference code itself
+(tests/golden/make_golden.py: the reference's src/model/model.py + train.train_epoch, and
+transformers' BertModel / ViTModel). CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import encoders as OE
+from oracle import fusion_head as OF
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def _t(a):
+    return torch.from_numpy(np.array(a))
+
+
+def _params(z, prefix):
+    return {k[len(prefix):]: _t(z[k]) for k in z.files if k.startswith(prefix)}
+
+
+def _close(a, b, tol=2e-5):
+    a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = (a - b).abs().max().item()
+    assert err <= tol * max(1.0, b.abs().max().item()), err
+
+
+@pytest.fixture(scope="module")
+def small():
+    return _load("fusion_small.npz")
+
+
+def test_fusion_small_eval_modes(small):
+    z = small
+    P = _params(z, "init/")
+    X = {k: _t(z[k]) for k in ("X_t", "X_i", "E_t", "E_i")}
+    with torch.no_grad():
+        (a, b), (c, d) = OF.model_forward(P, X["X_t"], X["X_i"], X["E_t"], X["E_i"], num_heads=4)
+        for n, y in zip(("tt", "ti", "it", "ii"), (a, b, c, d)):
+            _close(y, z[f"eval_{n}"])
+        _close(a, z["sdpa_tt"])  # SDPA branch == eager branch (layers.py:44-54)
+        (u, n1), (n2, n3) = OF.model_forward(P, X_t=X["X_t"], E_t=X["E_t"], num_heads=4)
+        assert n1 is None and n2 is None and n3 is None
+        _close(u, z["uni_tt"])
+        Pf = _params(z, "factify_init/")
+        y, none = OF.model_forward(Pf, X["X_t"], X["X_i"], X["E_t"], X["E_i"], num_heads=4, factify=True)
+        assert none is None
+        _close(y, z["factify_out"])
+        Pt = _params(z, "text_only_init/")
+        y, _ = OF.model_forward(Pt, X_t=X["X_t"], E_t=X["E_t"], num_heads=4, text_only=True)
+        _close(y, z["text_only_out"])
+
+
+def test_fusion_small_train_step_matches_reference_train_epoch(small):
+    """One step of train.py:123-188 (zero_grad, forward, sum of 4 CE, backward, AdamW lr=1e-4)."""
+    z = small
+    P = {k: v.clone().requires_grad_(True) for k, v in _params(z, "init/").items()}
+    X = {k: _t(z[k]) for k in ("X_t", "X_i", "E_t", "E_i")}
+    labels = _t(z["labels"])
+    out = OF.model_forward(P, X["X_t"], X["X_i"], X["E_t"], X["E_i"], num_heads=4)
+    total, per = OF.path_loss(out, labels)
+    _close(total, z["train_total_loss"])
+    for n, l in zip(("text_text", "text_image", "image_text", "image_image"), per):
+        _close(l, z[f"train_loss_{n}"])
+    total.backward()
+    names = [k for k, _ in json.loads(str(z["param_names"]))]
+    for k in names:
+        gk = "grad/" + k
+        if gk in z.files:
+            _close(P[k].grad, z[gk], 5e-5)
+        else:
+            assert P[k].grad is None, f"{k} should get no gradient (unused LayerNorm)"
+    assert sum("grad/" + k in z.files for k in names) == len(names) - 4  # text/image_self_ln2 w+b
+    opt = torch.optim.AdamW([P[k] for k in names], lr=1e-4)
+    opt.step()
+    for k in names:
+        _close(P[k].detach(), z["post/" + k], 1e-6)
+
+
+def test_fusion_full_dims_recipe():
+    z = _load("fusion_full.npz")
+    names = json.loads(str(z["param_names"]))
+    assert len(names) == 108  # the reference's 4-path state_dict
+    P = OF.init_params_like_reference(names, int(z["seed"]))
+    assert sum(v.numel() for v in P.values()) == int(z["n_params"]) == 4410892
+    with torch.no_grad():
+        (a, b), (c, d) = OF.model_forward(P, *(_t(z[k]) for k in ("X_t", "X_i", "E_t", "E_i")), num_heads=8)
+    for y, k in zip((a, b, c, d), ("tt", "ti", "it", "ii")):
+        _close(y, z[k], 1e-5)
+
+
+def test_bert_small():
+    z = _load("bert_small.npz")
+    cfg = json.loads(str(z["config"]))
+    P = {k: v.clone().requires_grad_(True) for k, v in _params(z, "param/").items()}
+    out = OE.bert_forward(P, _t(z["input_ids"]), _t(z["attention_mask"]), _t(z["token_type_ids"]),
+                          num_layers=cfg["num_hidden_layers"], num_heads=cfg["num_attention_heads"])
+    _close(out, z["out"], 2e-5)
+    (out * _t(z["R"])).sum().backward()
+    for k in P:
+        _close(P[k].grad, z["grad/" + k], 5e-5)
+
+
+def test_vit_small():
+    z = _load("vit_small.npz")
+    cfg = json.loads(str(z["config"]))
+    P = {k: v.clone().requires_grad_(True) for k, v in _params(z, "param/").items()}
+    out = OE.vit_forward(P, _t(z["pixel_values"]), num_layers=cfg["num_hidden_layers"],
+                         num_heads=cfg["num_attention_heads"], patch=cfg["patch_size"])
+    _close(out, z["out"], 2e-5)
+    (out * _t(z["R"])).sum().backward()
+    for k in P:
+        _close(P[k].grad, z["grad/" + k], 5e-5)
+
+
+def test_bert_vit_base_recipe():
+    z = _load("bert_base.npz")
+    P = OF.init_params_like_reference(json.loads(str(z["param_names"])), int(z["seed"]))
+    with torch.no_grad():
+        out = OE.bert_forward(P, _t(z["input_ids"]), _t(z["attention_mask"]), num_layers=12, num_heads=12)
+    _close(out, z["out"], 5e-5)
+    z = _load("vit_base.npz")
+    P = OF.init_params_like_reference(json.loads(str(z["param_names"])), int(z["seed"]))
+    with torch.no_grad():
+        out = OE.vit_forward(P, _t(z["pixel_values"]).float(), num_layers=12, num_heads=12)
+    _close(out, z["out"], 5e-5)
