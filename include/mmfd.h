@@ -100,7 +100,7 @@ int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, flo
 /* ------------------------------------------------------------------------------------------- */
 typedef struct mmfd_attn_args {
   int dtype;
-  int64_t B, H, Lq, Lk, D;         /* D in {32, 64} */
+  int64_t B, H, Lq, Lk, D;         /* D <= 64, D * element size a multiple of 16 B */
   float scale;
   const void* q; int64_t q_sb, q_st;
   const void* k; int64_t k_sb, k_st;
@@ -213,6 +213,9 @@ int mmfd_axpby(int dtype, int64_t n, float a, const void* x, float b, const void
 /* generic dropout (out = keep ? x/(1-p) : 0), index = element index. */
 int mmfd_dropout(int dtype, int64_t n, const void* x, void* out, float p, const uint64_t* seed,
                  uint64_t salt, mmfd_stream_t stream);
+/* out = dropout(dy) * act'(aux) over n contiguous elements (standalone layers.MLP backward) */
+int mmfd_act_bwd(int dtype, int64_t n, const void* dy, const void* aux, int act, float dropout_p,
+                 const uint64_t* seed, uint64_t salt, void* out, mmfd_stream_t stream);
 /* seed[0] += 1 (advances the step seed inside a captured graph) */
 int mmfd_seed_advance(uint64_t* seed, mmfd_stream_t stream);
 

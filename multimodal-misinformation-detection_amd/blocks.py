@@ -1,0 +1,167 @@
+"""Forward/backward building blocks shared by the fusion head and the encoders.
+
+Every function here only sequences kernel launches (kernels.py); there is no torch math. A
+`StepCtx` carries the per-call policy: activation dtype (fp32 parity mode / bf16 throughput mode),
+dropout probability and the device-resident step seed, the weight views in compute dtype and the
+parameter-gradient accumulators (first write overwrites, later writes accumulate with beta=1, so
+tensors used by several paths — the shared MLPs / Q projections of model.py:165-166,188-228 — sum
+their gradients inside the GEMM epilogue).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+
+class StepCtx:
+    def __init__(self, params: dict, dtype: torch.dtype, dropout_p: float = 0.0, seed: K.Seed | None = None,
+                 training: bool = False):
+        self.P = params          # name -> fp32 master tensor (nn.Parameter data)
+        self.dt = dtype
+        self.p = float(dropout_p) if training else 0.0
+        self.seed = seed
+        self.training = training
+        self._w = {}             # cached compute-dtype weights
+        self.grads = {}          # name -> fp32 grad tensor
+        self._written = set()
+
+    # ---- weights -------------------------------------------------------------------------------
+    def w(self, name):
+        """weight `name.weight` in compute dtype"""
+        key = name
+        t = self._w.get(key)
+        if t is None:
+            src = self.P[name + ".weight"]
+            t = src if self.dt == torch.float32 else K.cast(src, self.dt)
+            self._w[key] = t
+        return t
+
+    def b(self, name):
+        return self.P.get(name + ".bias")
+
+    def w_packed(self, names):
+        """row-concatenation of several nn.Linear weights (fused QKV / K|V GEMM) in compute dtype"""
+        key = "|".join(names)
+        t = self._w.get(key)
+        if t is None:
+            ws = [self.P[n + ".weight"] for n in names]
+            rows = sum(w.shape[0] for w in ws)
+            t = torch.empty((rows, ws[0].shape[1]), device=ws[0].device, dtype=self.dt)
+            r = 0
+            for w in ws:
+                K.cast(w, self.dt, out=t[r:r + w.shape[0]])
+                r += w.shape[0]
+            bs = [self.P[n + ".bias"] for n in names]
+            bt = torch.empty(rows, device=ws[0].device, dtype=torch.float32)
+            r = 0
+            for bb in bs:
+                K.cast(bb, torch.float32, out=bt[r:r + bb.shape[0]])
+                r += bb.shape[0]
+            self._w[key] = t
+            self._w[key + "#bias"] = bt
+        return t, self._w[key + "#bias"]
+
+    # ---- dropout -------------------------------------------------------------------------------
+    def drop(self, site):
+        """(p, seed, salt) kwargs for a dropout site; p=0 when not training."""
+        if self.p <= 0.0:
+            return {}
+        return dict(dropout_p=self.p, seed=self.seed, salt=K.salt_of(site))
+
+    # ---- gradients -----------------------------------------------------------------------------
+    def grad_slot(self, pname, shape):
+        """(tensor, beta) for accumulating into the gradient of parameter `pname`."""
+        g = self.grads.get(pname)
+        if g is None:
+            g = torch.empty(shape, device=self.P[pname].device, dtype=torch.float32)
+            self.grads[pname] = g
+            return g, 0.0
+        return g, 1.0
+
+    def lin_grads(self, names, dy2d, x2d):
+        """dW = dy^T x (fp32, accumulate), db = colsum(dy); `names` are the row blocks of dy."""
+        if len(names) == 1:
+            n = names[0]
+            g, beta = self.grad_slot(n + ".weight", self.P[n + ".weight"].shape)
+            K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta)
+            gb, bb = self.grad_slot(n + ".bias", self.P[n + ".bias"].shape)
+            K.colsum(dy2d, out=gb, beta=bb)
+            return
+        r = 0
+        for n in names:
+            rows = self.P[n + ".weight"].shape[0]
+            self.lin_grads([n], dy2d[:, r:r + rows], x2d)
+            r += rows
+
+
+def as2d(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+# -------------------------------------------------------------------------------------------------
+# linear
+# -------------------------------------------------------------------------------------------------
+def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=None, drop_site=None,
+           out_dtype=None):
+    W = ctx.w(name)
+    aux = None
+    if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
+        aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
+    y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,
+               **(ctx.drop(drop_site) if drop_site else {}))
+    return y, aux
+
+
+def linear_packed(ctx: StepCtx, x2d, names):
+    W, b = ctx.w_packed(names)
+    return K.gemm(x2d, W, bias=b)
+
+
+def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None):
+    W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
+    return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
+                  **(ctx.drop(drop_site) if drop_site else {}))
+
+
+# -------------------------------------------------------------------------------------------------
+# LayerNorm
+# -------------------------------------------------------------------------------------------------
+def layernorm(ctx: StepCtx, x2d, name, eps):
+    return K.layernorm_fwd(x2d, ctx.P[name + ".weight"], ctx.P[name + ".bias"], eps)
+
+
+def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, drop_site=None):
+    """Returns (dx, dx_dropped or None). Gamma/beta grads accumulate into ctx.grads."""
+    gw, bw = ctx.grad_slot(name + ".weight", ctx.P[name + ".weight"].shape)
+    gb, bb = ctx.grad_slot(name + ".bias", ctx.P[name + ".bias"].shape)
+    assert bw == bb
+    dd = None
+    kw = {}
+    if drop_site is not None and ctx.p > 0:
+        dd = torch.empty_like(dy2d)
+        kw = dict(dx_drop=dd, dropout_p=ctx.p, seed=ctx.seed, salt=K.salt_of(drop_site))
+    dx = K.layernorm_bwd(dy2d, x2d, ctx.P[name + ".weight"], mean, rstd, dx_add=dx_add, dgamma=gw, dbeta=gb,
+                         beta_acc=bw, **kw)
+    return dx, dd
+
+
+# -------------------------------------------------------------------------------------------------
+# MLP block:  y = LN(a + drop(W2 drop(gelu(W1 a + b1)) + b2))     (layers.py:12-18 + model.py:109)
+# -------------------------------------------------------------------------------------------------
+def mlp_ln_fwd(ctx: StepCtx, a2d, mlp, ln, site, eps=1e-5, w1=".net.0", w2=".net.3"):
+    h, pre = linear(ctx, a2d, mlp + w1, act=K.ACT_GELU, keep_aux=True, drop_site=site + ".h")
+    s, _ = linear(ctx, h, mlp + w2, residual=a2d, drop_site=site + ".out")
+    y, mean, rstd = layernorm(ctx, s, ln, eps)
+    return y, (a2d, h, pre, s, mean, rstd, mlp, ln, site, w1, w2)
+
+
+def mlp_ln_bwd(ctx: StepCtx, dy2d, st):
+    a2d, h, pre, s, mean, rstd, mlp, ln, site, w1, w2 = st
+    ds, ds_drop = layernorm_bwd(ctx, dy2d, s, ln, mean, rstd, drop_site=site + ".out")
+    g_out = ds_drop if ds_drop is not None else ds
+    ctx.lin_grads([mlp + w2], g_out, h)
+    dpre = linear_dx(ctx, g_out, mlp + w2, act=K.ACT_GELU_BWD, aux=pre, drop_site=site + ".h")
+    ctx.lin_grads([mlp + w1], dpre, a2d)
+    linear_dx(ctx, dpre, mlp + w1, out=ds, beta=1.0)  # da = ds + dpre W1
+    return ds

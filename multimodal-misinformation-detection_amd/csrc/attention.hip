@@ -23,6 +23,7 @@ namespace {
 
 struct AttnP {
   int64_t B, H, Lq, Lk;
+  int D;  // real head dim (<= the template's padded D; padding columns are zero)
   float scale;
   const void* q; int64_t q_sb, q_st;
   const void* k; int64_t k_sb, k_st;
@@ -73,12 +74,12 @@ __device__ __forceinline__ int tr_chunk(int r, int c) {
 // stage 64 rows [row0, row0+64) of a (token-strided) head slice into an image
 template <typename T, int D, bool TR>
 __device__ __forceinline__ void stage_rows(char* lds, const T* __restrict__ base, int64_t st, int64_t row0,
-                                           int64_t nrows, int tid) {
+                                           int64_t nrows, int tid, int dreal) {
   constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
   for (int c = tid; c < 64 * NCH; c += 256) {
     const int r = c / NCH, ch = c % NCH;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (row0 + r < nrows) v = *reinterpret_cast<const uint4*>(base + (row0 + r) * st + ch * EPC);
+    if (row0 + r < nrows && ch * EPC < dreal) v = *reinterpret_cast<const uint4*>(base + (row0 + r) * st + ch * EPC);
     const int off = TR ? (r * AT<T, D>::RB + (tr_chunk<T, D>(r, ch) << 4)) : row_off<T, D>(r, ch);
     *reinterpret_cast<uint4*>(lds + off) = v;
   }
@@ -137,12 +138,13 @@ __device__ __forceinline__ uint4 pack_acc(const f32x4* s, int c) {
 // per-lane 16-B operand chunks of one row (query or key) held in registers
 template <typename T, int D>
 __device__ __forceinline__ void load_row_regs(uint4* f, const T* __restrict__ base, int64_t st,
-                                              int64_t row, int64_t nrows, int lane) {
+                                              int64_t row, int64_t nrows, int lane, int dreal) {
   const int g = lane >> 4;
 #pragma unroll
   for (int kc = 0; kc < AT<T, D>::KCH; ++kc) {
     f[kc] = make_uint4(0, 0, 0, 0);
-    if (row < nrows) f[kc] = *reinterpret_cast<const uint4*>(base + row * st + (kc * 4 + g) * AT<T, D>::EPC);
+    const int col = (kc * 4 + g) * AT<T, D>::EPC;
+    if (row < nrows && col < dreal) f[kc] = *reinterpret_cast<const uint4*>(base + row * st + col);
   }
 }
 
@@ -165,13 +167,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
-  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
-  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
-  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
   const int64_t myq = q0 + li;
 
   uint4 qf[C::KCH];
-  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane);
+  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
 
   float m = -INFINITY, lsum = 0.f;
@@ -181,8 +183,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
 
   for (int64_t k0 = 0; k0 < p.Lk; k0 += 64) {
     __syncthreads();
-    stage_rows<T, D, false>(k_img, kb, p.k_st, k0, p.Lk, tid);
-    stage_rows<T, D, true>(v_img, vb, p.v_st, k0, p.Lk, tid);
+    stage_rows<T, D, false>(k_img, kb, p.k_st, k0, p.Lk, tid, p.D);
+    stage_rows<T, D, true>(v_img, vb, p.v_st, k0, p.Lk, tid, p.D);
     __syncthreads();
 
     f32x4 s[4];
@@ -242,7 +244,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
     }
   }
 
-  T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * D;
+  T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float lr = __shfl(lsum, 4 * g + r, 64);
@@ -250,7 +252,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
     const float inv = 1.0f / lr;
     if (q < p.Lq) {
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
+      for (int d = 0; d < C::DT; ++d)
+        if (d * 16 + li < p.D) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
     }
   }
   if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = m + __logf(lsum);
@@ -270,10 +273,12 @@ __global__ void attn_delta_kernel(AttnP p) {
   float s = 0.f;
   if (row < total) {
     const int64_t q = row % p.Lq, bh = row / p.Lq, b = bh / p.H, h = bh % p.H;
-    const T* o = reinterpret_cast<const T*>(p.o) + b * p.o_sb + q * p.o_st + h * D + ch * AT<T, D>::EPC;
-    const T* d = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + q * p.do_st + h * D + ch * AT<T, D>::EPC;
+    if (ch * AT<T, D>::EPC < p.D) {
+      const T* o = reinterpret_cast<const T*>(p.o) + b * p.o_sb + q * p.o_st + h * p.D + ch * AT<T, D>::EPC;
+      const T* d = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + q * p.do_st + h * p.D + ch * AT<T, D>::EPC;
 #pragma unroll
-    for (int j = 0; j < AT<T, D>::EPC; ++j) s += to_f32(o[j]) * to_f32(d[j]);
+      for (int j = 0; j < AT<T, D>::EPC; ++j) s += to_f32(o[j]) * to_f32(d[j]);
+    }
   }
 #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -297,15 +302,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
   const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t k0 = (int64_t)blockIdx.x * 64 + wave * 16;
   const int64_t mykey = k0 + li;
-  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
-  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
-  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
-  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * D;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
 
   uint4 kf[C::KCH], vf[C::KCH];
-  load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane);
-  load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane);
+  load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
+  load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
 
   f32x4 dk[C::DT], dv[C::DT];
 #pragma unroll
@@ -313,10 +318,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
 
   for (int64_t qs0 = 0; qs0 < p.Lq; qs0 += 64) {
     __syncthreads();
-    stage_rows<T, D, false>(q_row, qb, p.q_st, qs0, p.Lq, tid);
-    stage_rows<T, D, true>(q_tr, qb, p.q_st, qs0, p.Lq, tid);
-    stage_rows<T, D, false>(do_row, dob, p.do_st, qs0, p.Lq, tid);
-    stage_rows<T, D, true>(do_tr, dob, p.do_st, qs0, p.Lq, tid);
+    stage_rows<T, D, false>(q_row, qb, p.q_st, qs0, p.Lq, tid, p.D);
+    stage_rows<T, D, true>(q_tr, qb, p.q_st, qs0, p.Lq, tid, p.D);
+    stage_rows<T, D, false>(do_row, dob, p.do_st, qs0, p.Lq, tid, p.D);
+    stage_rows<T, D, true>(do_tr, dob, p.do_st, qs0, p.Lq, tid, p.D);
     if (tid < 64) {
       const int64_t q = qs0 + tid;
       s_lse[tid] = q < p.Lq ? p.lse[bh * p.Lq + q] : INFINITY;
@@ -364,14 +369,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
     }
   }
 
-  T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * D;
-  T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * D;
+  T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * p.D;
+  T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int64_t key = k0 + 4 * g + r;
     if (key < p.Lk) {
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
+        if (d * 16 + li >= p.D) continue;
         T* pk = dkb + key * p.dk_st + d * 16 + li;
         T* pv = dvb + key * p.dv_st + d * 16 + li;
         float vk = dk[d][r] * p.scale, vv = dv[d][r];
@@ -397,15 +403,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
   const int64_t bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
   const int64_t myq = q0 + li;
-  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * D;
-  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * D;
-  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * D;
-  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * D;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
 
   uint4 qf[C::KCH], dof[C::KCH];
-  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane);
-  load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane);
+  load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+  load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
   const float lse = myq < p.Lq ? p.lse[bh * p.Lq + myq] : INFINITY;
   const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
 
@@ -415,9 +421,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 
   for (int64_t k0 = 0; k0 < p.Lk; k0 += 64) {
     __syncthreads();
-    stage_rows<T, D, false>(k_row, kb, p.k_st, k0, p.Lk, tid);
-    stage_rows<T, D, true>(k_tr, kb, p.k_st, k0, p.Lk, tid);
-    stage_rows<T, D, false>(v_row, vb, p.v_st, k0, p.Lk, tid);
+    stage_rows<T, D, false>(k_row, kb, p.k_st, k0, p.Lk, tid, p.D);
+    stage_rows<T, D, true>(k_tr, kb, p.k_st, k0, p.Lk, tid, p.D);
+    stage_rows<T, D, false>(v_row, vb, p.v_st, k0, p.Lk, tid, p.D);
     __syncthreads();
 
     f32x4 ds[4];
@@ -454,13 +460,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
     }
   }
 
-  T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * D;
+  T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int64_t q = q0 + 4 * g + r;
     if (q < p.Lq) {
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
+        if (d * 16 + li >= p.D) continue;
         T* pq = dqb + q * p.dq_st + d * 16 + li;
         float vq = dq[d][r] * p.scale;
         if (p.acc_dq) vq += to_f32(*pq);
@@ -472,10 +479,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 
 int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "attn: bad dtype");
-  MMFD_CHECK_ARG(a.D == 32 || a.D == 64, "attn: head_dim %lld unsupported (32 or 64)", (long long)a.D);
+  MMFD_CHECK_ARG(a.D > 0 && a.D <= 64, "attn: head_dim %lld unsupported (<= 64)", (long long)a.D);
   MMFD_CHECK_ARG(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attn: bad shape");
   MMFD_CHECK_ARG(a.q && a.k && a.v && a.o && a.lse, "attn: null pointer");
   const int epc = a.dtype == MMFD_BF16 ? 8 : 4;
+  MMFD_CHECK_ARG(a.D % epc == 0, "attn: head_dim*element_size must be a multiple of 16 bytes");
   auto al = [&](const void* ptr, int64_t sb, int64_t st) {
     return ((uintptr_t)ptr & 15) == 0 && sb % epc == 0 && st % epc == 0;
   };
@@ -488,7 +496,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
     MMFD_CHECK_ARG(al(a.dout, a.do_sb, a.do_st), "attn_bwd: dout alignment");
     MMFD_CHECK_ARG(a.d_rel_bias == nullptr, "attn_bwd: relative-bias gradient not supported");
   }
-  p.B = a.B; p.H = a.H; p.Lq = a.Lq; p.Lk = a.Lk; p.scale = a.scale;
+  p.B = a.B; p.H = a.H; p.Lq = a.Lq; p.Lk = a.Lk; p.scale = a.scale; p.D = (int)a.D;
   p.q = a.q; p.q_sb = a.q_sb; p.q_st = a.q_st;
   p.k = a.k; p.k_sb = a.k_sb; p.k_st = a.k_st;
   p.v = a.v; p.v_sb = a.v_sb; p.v_st = a.v_st;
@@ -534,8 +542,8 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == MMFD_BF16) { if (a->D == 64) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
-  else { if (a->D == 64) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
+  if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
+  else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_fwd");
   return 0;
 }
@@ -547,8 +555,8 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == MMFD_BF16) { if (a->D == 64) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
-  else { if (a->D == 64) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
+  if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
+  else { if (a->D > 32) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_bwd");
   return 0;
 }

@@ -64,6 +64,21 @@ __global__ void dropout_kernel(int64_t n, const T* __restrict__ x, T* __restrict
 
 __global__ void seed_advance_kernel(uint64_t* seed) { seed[0] += 1; }
 
+template <typename T>
+__global__ void act_bwd_kernel(int64_t n, int64_t width, const T* __restrict__ dy, const T* __restrict__ aux, int act,
+                               float p, uint32_t thr, const uint64_t* __restrict__ seedp, uint64_t salt, T* __restrict__ out) {
+  const uint64_t seed = p > 0.f ? *seedp : 0ull;
+  const float sc = 1.0f / (1.0f - p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float z = to_f32(dy[i]);
+    if (p > 0.f) z = (mmfd_hash(seed, salt, (uint64_t)i) < thr) ? 0.f : z * sc;
+    const float a = to_f32(aux[i]);
+    if (act == MMFD_ACT_GELU) z *= gelu_grad_f(a);
+    else if (act == MMFD_ACT_RELU) z = a > 0.f ? z : 0.f;
+    out[i] = from_f32<T>(z);
+  }
+}
+
 }  // namespace
 
 extern "C" int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream) {
@@ -112,6 +127,24 @@ extern "C" int mmfd_dropout(int dtype, int64_t n, const void* x, void* out, floa
   else
     hipLaunchKernelGGL((dropout_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const float*)x, (float*)out, p, thr, seed, salt);
   MMFD_CHECK_LAUNCH("dropout");
+  return 0;
+}
+
+extern "C" int mmfd_act_bwd(int dtype, int64_t n, const void* dy, const void* aux, int act, float dropout_p,
+                            const uint64_t* seed, uint64_t salt, void* out, mmfd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MMFD_CHECK_ARG(act == MMFD_ACT_GELU || act == MMFD_ACT_RELU || act == MMFD_ACT_NONE, "act_bwd: bad act");
+  MMFD_CHECK_ARG(dropout_p <= 0.f || seed, "act_bwd: dropout needs seed");
+  if (n == 0) return 0;
+  const float p = dropout_p > 0.f ? dropout_p : 0.f;
+  const uint32_t thr = mmfd_drop_threshold(p);
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((act_bwd_kernel<bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, (int64_t)0, (const bf16*)dy,
+                       (const bf16*)aux, act, p, thr, seed, salt, (bf16*)out);
+  else
+    hipLaunchKernelGGL((act_bwd_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, n, (int64_t)0, (const float*)dy,
+                       (const float*)aux, act, p, thr, seed, salt, (float*)out);
+  MMFD_CHECK_LAUNCH("act_bwd");
   return 0;
 }
 

@@ -1,0 +1,277 @@
+"""The fusion classifier (reference src/model/model.py + layers.py) as an explicit forward and a
+hand-written backward over HIP kernels.
+
+Forward follows model.py:426-468 exactly, including its quirks:
+  * the representation's "cross" attention uses the unprojected H as Q against the same
+    modality's K/V (model.py:106, 115);
+  * no padding mask anywhere in the head (layers.py:51); mean pooling over all positions;
+  * text_self_ln2 / image_self_ln2 are only used by the unimodal branches (model.py:89, 99).
+MI355X-specific restructuring (same values): Q/K/V of a modality are one fused GEMM (N = 3E); the
+evidence K and V are one GEMM (N = 2E) computed once per modality instead of once per path, and
+the per-path Q projections once per claim modality (model.py:188/201, 189-190/215-216, 202-203/
+228-229, 214/227 recompute identical values); every attention output projection carries the
+residual add in its GEMM epilogue; dropout masks are generated in the epilogues.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import blocks as Bk
+from . import kernels as K
+
+
+class HeadConfig:
+    def __init__(self, embed_dim, num_heads, factify=False, text_only=False, ln_eps=1e-5):
+        self.E = embed_dim
+        self.H = num_heads
+        self.factify = factify
+        self.text_only = text_only
+        self.eps = ln_eps
+
+
+# -------------------------------------------------------------------------------------------------
+# attention block: y = LN(res + out_proj(MHA(q, k, v)))
+# -------------------------------------------------------------------------------------------------
+def _attn_ln_fwd(ctx, cfg, q, k, v, res2d, out_name, ln_name, site):
+    B, Lq, _ = q.shape
+    o, lse = K.attn_fwd(q, k, v, cfg.H, **ctx.drop(site + ".attn"))
+    s, _ = Bk.linear(ctx, Bk.as2d(o), out_name, residual=res2d)
+    y, mean, rstd = Bk.layernorm(ctx, s, ln_name, cfg.eps)
+    return y, (q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site)
+
+
+def _attn_ln_bwd(ctx, cfg, dy2d, st, *, dq=None, acc_dq=False, dk=None, dv=None, acc_dkv=False):
+    """Returns ds (the gradient of the residual input); writes/accumulates dq, dk, dv."""
+    q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = st
+    ds, _ = Bk.layernorm_bwd(ctx, dy2d, s, ln_name, mean, rstd)
+    ctx.lin_grads([out_name], ds, Bk.as2d(o))
+    do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
+    K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dq, dk=dk, dv=dv, accumulate_dq=acc_dq, accumulate_dkv=acc_dkv,
+               **ctx.drop(site + ".attn"))
+    return ds
+
+
+# -------------------------------------------------------------------------------------------------
+# representation (model.py:56-121)
+# -------------------------------------------------------------------------------------------------
+def _repr_modality_fwd(ctx, cfg, Xin, m, unimodal):
+    r = "representation."
+    B, L, _ = Xin.shape
+    E = cfg.E
+    X, _ = Bk.linear(ctx, Bk.as2d(Xin), r + f"{m}_proj")
+    qkv = Bk.linear_packed(ctx, X, [r + f"{m}_WQ", r + f"{m}_WK", r + f"{m}_WV"]).view(B, L, 3 * E)
+    q, k, v = qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]
+    Hh, st1 = _attn_ln_fwd(ctx, cfg, q, k, v, X, r + f"{m}_self_attn_out", r + f"{m}_self_ln1", r + f"{m}.self")
+    if unimodal:  # model.py:83-100: self-attention, then MLP + self_ln2
+        Y, st3 = Bk.mlp_ln_fwd(ctx, Hh, r + f"{m}_mlp", r + f"{m}_self_ln2", r + f"{m}.mlp", cfg.eps)
+        return Y.view(B, L, E), dict(Xin=Xin, X=X, qkv=qkv, st1=st1, st2=None, st3=st3, m=m)
+    Hv = Hh.view(B, L, E)
+    C, st2 = _attn_ln_fwd(ctx, cfg, Hv, k, v, Hh, r + f"{m}_cross_attn_out", r + f"{m}_cross_ln1", r + f"{m}.cross")
+    Y, st3 = Bk.mlp_ln_fwd(ctx, C, r + f"{m}_mlp", r + f"{m}_cross_ln2", r + f"{m}.mlp", cfg.eps)
+    return Y.view(B, L, E), dict(Xin=Xin, X=X, qkv=qkv, st1=st1, st2=st2, st3=st3, m=m)
+
+
+def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin):
+    r = "representation."
+    m = st["m"]
+    E = cfg.E
+    qkv = st["qkv"]
+    B, L, _ = qkv.shape
+    dqkv = torch.empty_like(qkv)
+    dC = Bk.mlp_ln_bwd(ctx, dY2d, st["st3"])
+    if st["st2"] is not None:
+        q2, k2, v2, o2, lse2, s2, mean2, rstd2, out2, ln2, site2 = st["st2"]
+        ds2, _ = Bk.layernorm_bwd(ctx, dC, s2, ln2, mean2, rstd2)      # dH (residual part)
+        ctx.lin_grads([out2], ds2, Bk.as2d(o2))
+        do2 = Bk.linear_dx(ctx, ds2, out2).view(o2.shape)
+        # dq of the cross attention goes straight into dH (= ds2), dk/dv start dQKV's K|V blocks
+        K.attn_bwd(q2, k2, v2, o2, lse2, do2, cfg.H, dq=ds2.view(B, L, E), dk=dqkv[..., E:2 * E],
+                   dv=dqkv[..., 2 * E:], accumulate_dq=True, accumulate_dkv=False, **ctx.drop(site2 + ".attn"))
+        dX = _attn_ln_bwd(ctx, cfg, ds2, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:],
+                          acc_dkv=True)
+    else:
+        dX = _attn_ln_bwd(ctx, cfg, dC, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:])
+    dqkv2 = Bk.as2d(dqkv)
+    names = [r + f"{m}_WQ", r + f"{m}_WK", r + f"{m}_WV"]
+    ctx.lin_grads(names, dqkv2, st["X"])
+    Wp, _ = ctx.w_packed(names)
+    Bk.linear_dx(ctx, dqkv2, Wp, out=dX, beta=1.0)  # dX += dQKV [WQ;WK;WV]
+    ctx.lin_grads([r + f"{m}_proj"], dX, Bk.as2d(st["Xin"]))
+    return Bk.linear_dx(ctx, dX, r + f"{m}_proj").view(st["Xin"].shape) if need_dxin else None
+
+
+# -------------------------------------------------------------------------------------------------
+# evidence conditioning (model.py:172-237)
+# -------------------------------------------------------------------------------------------------
+PATHS = [  # (claim modality, evidence modality, path tag, out proj, ln prefix)
+    ("text", "text", "tt", "text_text"),
+    ("text", "image", "ti", "text_image"),
+    ("image", "text", "it", "image_text"),
+    ("image", "image", "ii", "image_image"),
+]
+
+
+def _cond_fwd(ctx, cfg, Hs, Es):
+    c = "cross_attn."
+    E = cfg.E
+    Q, KV, out, st = {}, {}, {}, {}
+    for m in ("text", "image"):
+        if Hs.get(m) is not None and any(Es.get(e) is not None for e in ("text", "image")):
+            B, L, _ = Hs[m].shape
+            Q[m] = Bk.linear(ctx, Bk.as2d(Hs[m]), c + f"{m}_WQ")[0].view(B, L, E)
+        if Es.get(m) is not None and any(Hs.get(x) is not None for x in ("text", "image")):
+            B, L, _ = Es[m].shape
+            KV[m] = Bk.linear_packed(ctx, Bk.as2d(Es[m]), [c + f"{m}_evidence_key", c + f"{m}_evidence_value"]
+                                     ).view(B, L, 2 * E)
+    for hm, em, tag, name in PATHS:
+        if Hs.get(hm) is None or Es.get(em) is None:
+            continue
+        kv = KV[em]
+        a, s1 = _attn_ln_fwd(ctx, cfg, Q[hm], kv[..., :E], kv[..., E:], Bk.as2d(Hs[hm]), c + f"{name}_out",
+                             c + f"{name}_ln1", c + tag)
+        S, s2 = Bk.mlp_ln_fwd(ctx, a, c + f"{hm}_mlp", c + f"{name}_ln2", c + tag + ".mlp", cfg.eps)
+        out[tag] = S.view(Hs[hm].shape)
+        st[tag] = (s1, s2)
+    return out, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
+
+
+def _cond_bwd(ctx, cfg, dS, cst, need_dE):
+    """dS: tag -> [B, L, E] grads. Returns (dH per claim modality (2-D), dE per evidence modality)."""
+    c = "cross_attn."
+    E = cfg.E
+    dH, dQ, dKV = {}, {}, {}
+    for hm, em, tag, name in PATHS:
+        if tag not in cst["st"]:
+            continue
+        s1, s2 = cst["st"][tag]
+        da = Bk.mlp_ln_bwd(ctx, Bk.as2d(dS[tag]), s2)
+        q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = s1
+        ds, _ = Bk.layernorm_bwd(ctx, da, s, ln_name, mean, rstd)
+        ctx.lin_grads([out_name], ds, Bk.as2d(o))
+        do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
+        # residual gradient into H, summed over the claim modality's two paths
+        if hm in dH:
+            K.axpby(1.0, dH[hm], 1.0, ds, out=dH[hm])
+        else:
+            dH[hm] = ds
+        first_q = hm not in dQ
+        first_kv = em not in dKV
+        if first_q:
+            dQ[hm] = torch.empty_like(q)
+        if first_kv:
+            dKV[em] = torch.empty_like(cst["KV"][em])
+        K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dQ[hm], dk=dKV[em][..., :E], dv=dKV[em][..., E:],
+                   accumulate_dq=not first_q, accumulate_dkv=not first_kv, **ctx.drop(site + ".attn"))
+    for hm, dq in dQ.items():
+        dq2 = Bk.as2d(dq)
+        ctx.lin_grads([c + f"{hm}_WQ"], dq2, Bk.as2d(cst["Hs"][hm]))
+        Bk.linear_dx(ctx, dq2, c + f"{hm}_WQ", out=dH[hm], beta=1.0)
+    dE = {}
+    for em, dkv in dKV.items():
+        names = [c + f"{em}_evidence_key", c + f"{em}_evidence_value"]
+        dkv2 = Bk.as2d(dkv)
+        ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]))
+        if need_dE.get(em):
+            Wp, _ = ctx.w_packed(names)
+            dE[em] = Bk.linear_dx(ctx, dkv2, Wp).view(cst["Es"][em].shape)
+    return dH, dE
+
+
+# -------------------------------------------------------------------------------------------------
+# classifiers (model.py:240-347, 393-403)
+# -------------------------------------------------------------------------------------------------
+def _mlp_head_fwd(ctx, x2d, name, n_hidden, site):
+    acts = [x2d]
+    pres = []
+    idx = 0
+    h = x2d
+    for layer in range(n_hidden):
+        h, pre = Bk.linear(ctx, h, f"{name}.{idx}", act=K.ACT_RELU, keep_aux=True, drop_site=f"{site}.d{layer}")
+        acts.append(h)
+        pres.append(pre)
+        idx += 3
+    y, _ = Bk.linear(ctx, h, f"{name}.{idx}", out_dtype=torch.float32)
+    return y, (acts, pres, name, n_hidden, site)
+
+
+def _mlp_head_bwd(ctx, dy, st):
+    acts, pres, name, n_hidden, site = st
+    g = dy if ctx.dt == torch.float32 else K.cast(dy, ctx.dt)
+    idx = 3 * n_hidden
+    ctx.lin_grads([f"{name}.{idx}"], g, acts[-1])
+    for layer in reversed(range(n_hidden)):
+        # d(pre) = dX(next) * relu'(pre) * dropout mask
+        g = Bk.linear_dx(ctx, g, f"{name}.{idx}", act=K.ACT_RELU_BWD, aux=pres[layer], drop_site=f"{site}.d{layer}")
+        idx -= 3
+        ctx.lin_grads([f"{name}.{idx}"], g, acts[layer])
+    return Bk.linear_dx(ctx, g, f"{name}.{idx}")
+
+
+CLS_NAMES = {"tt": "mlp_text_given_text", "ti": "mlp_text_given_image", "it": "mlp_image_given_text",
+             "ii": "mlp_image_given_image"}
+
+
+# -------------------------------------------------------------------------------------------------
+# whole head
+# -------------------------------------------------------------------------------------------------
+def head_forward(ctx, cfg: HeadConfig, X_t, X_i, E_t, E_i):
+    """Returns (outputs, state). outputs: dict tag -> fp32 logits ('pred' for factify/text_only)."""
+    dt = ctx.dt
+    cast_in = lambda x: None if x is None else (x if x.dtype == dt else K.cast(x, dt))  # noqa: E731
+    X_t, X_i, E_t, E_i = (cast_in(x) for x in (X_t, X_i, E_t, E_i))
+    if cfg.text_only:
+        X_i = E_i = None
+    Hs, rst = {}, {}
+    uni = (X_t is None) != (X_i is None) or cfg.text_only
+    for m, x in (("text", X_t), ("image", X_i)):
+        if x is not None:
+            Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, x, m, unimodal=uni)
+    S, cst = _cond_fwd(ctx, cfg, Hs, {"text": E_t, "image": E_i})
+    pooled, hst, outs = {}, {}, {}
+    if cfg.text_only:
+        p = K.seq_mean_fwd(S["tt"])
+        outs["pred"], hst["pred"] = _mlp_head_fwd(ctx, p, "text_classifier", 2, "text_classifier")
+        pooled["tt"] = p
+    elif cfg.factify:
+        tags = [t for t in ("tt", "ti", "it", "ii") if t in S]
+        B = S[tags[0]].shape[0]
+        cat = torch.empty((B, cfg.E * len(tags)), device=S[tags[0]].device, dtype=dt)
+        for j, t in enumerate(tags):
+            K.seq_mean_fwd(S[t], out=cat[:, j * cfg.E:(j + 1) * cfg.E])
+        outs["pred"], hst["pred"] = _mlp_head_fwd(ctx, cat, "classifier.unified_mlp", 2, "classifier.unified")
+        hst["tags"] = tags
+    else:
+        for t in ("tt", "ti", "it", "ii"):
+            if t in S:
+                p = K.seq_mean_fwd(S[t])
+                name = "classifier." + CLS_NAMES[t]
+                outs[t], hst[t] = _mlp_head_fwd(ctx, p, name, 1, name)
+    state = dict(rst=rst, cst=cst, S=S, hst=hst, shapes={m: x.shape for m, x in (("text", X_t), ("image", X_i))
+                                                          if x is not None})
+    return outs, state
+
+
+def head_backward(ctx, cfg: HeadConfig, douts, state, need_dX=(True, True), need_dE=(True, True)):
+    """douts: dict tag -> fp32 grad of logits. Returns dX_t, dX_i, dE_t, dE_i (compute dtype or None)."""
+    S = state["S"]
+    hst = state["hst"]
+    dS = {}
+    if cfg.text_only or cfg.factify:
+        dcat = _mlp_head_bwd(ctx, douts["pred"], hst["pred"])
+        if cfg.text_only:
+            dS["tt"] = K.seq_mean_bwd(dcat, S["tt"].shape[1])
+        else:
+            for j, t in enumerate(hst["tags"]):
+                dS[t] = K.seq_mean_bwd(dcat[:, j * cfg.E:(j + 1) * cfg.E], S[t].shape[1])
+    else:
+        for t, st in hst.items():
+            dp = _mlp_head_bwd(ctx, douts[t], st)
+            dS[t] = K.seq_mean_bwd(dp, S[t].shape[1])
+    need_e = {"text": need_dE[0], "image": need_dE[1]}
+    dH, dE = _cond_bwd(ctx, cfg, dS, state["cst"], need_e)
+    dX = {}
+    for m, st in state["rst"].items():
+        need = need_dX[0] if m == "text" else need_dX[1]
+        if m in dH:
+            dX[m] = _repr_modality_bwd(ctx, cfg, dH[m], st, need)
+    return dX.get("text"), dX.get("image"), dE.get("text"), dE.get("image")

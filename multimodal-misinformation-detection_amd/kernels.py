@@ -113,6 +113,7 @@ SIGNATURES = {
     "mmfd_axpby": (_I, [_I, _I64, _F, _VP, _F, _VP, _VP, _VP]),
     "mmfd_dropout": (_I, [_I, _I64, _VP, _VP, _F, _VP, _U64, _VP]),
     "mmfd_seed_advance": (_I, [_VP, _VP]),
+    "mmfd_act_bwd": (_I, [_I, _I64, _VP, _VP, _I, _F, _VP, _U64, _VP, _VP]),
 }
 
 _lib = None
@@ -190,6 +191,14 @@ class Seed:
 
     def set(self, value: int):
         self.t.fill_(value)
+
+    def fork(self):
+        """Snapshot of the current value for one forward/backward pair (the kernels read the seed
+        at launch time), then advance this seed for the next forward."""
+        s = Seed.__new__(Seed)
+        s.t = self.t.clone()
+        self.advance()
+        return s
 
 
 # ------------------------------------------------------------------------------------------------
@@ -428,8 +437,11 @@ def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None):
     return loss, dl
 
 
-def cast(x, dtype):
-    out = torch.empty(x.shape, device=x.device, dtype=dtype)
+def cast(x, dtype, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    elif out.dtype != dtype or out.numel() != x.numel() or not out.is_contiguous():
+        raise ValueError("cast: out must be a contiguous tensor of the target dtype and size")
     if x.numel():
         _check(lib().mmfd_cast(dtype_code(x.dtype), dtype_code(dtype), x.numel(), _ptr(x.contiguous()), _ptr(out),
                                _stream()), "mmfd_cast")
@@ -447,6 +459,14 @@ def dropout(x, p, seed, salt, out=None):
     out = out if out is not None else torch.empty_like(x)
     _check(lib().mmfd_dropout(dtype_code(x.dtype), x.numel(), _ptr(x), _ptr(out), float(p), seed.ptr(),
                               int(salt) & 0xFFFFFFFFFFFFFFFF, _stream()), "mmfd_dropout")
+    return out
+
+
+def act_bwd(dy, aux, act, dropout_p=0.0, seed=None, salt=0, out=None):
+    out = out if out is not None else torch.empty_like(dy)
+    _check(lib().mmfd_act_bwd(dtype_code(dy.dtype), dy.numel(), _ptr(dy), _ptr(aux), int(act), float(dropout_p),
+                              seed.ptr() if seed is not None else None, int(salt) & 0xFFFFFFFFFFFFFFFF, _ptr(out),
+                              _stream()), "mmfd_act_bwd")
     return out
 
 

@@ -51,3 +51,22 @@ def keep_mask(seed: int, salt: int, shape, p: float):
     n = int(np.prod(shape))
     h = dropout_hash(seed, salt, np.arange(n, dtype=np.uint64))
     return (h >= np.uint32(drop_threshold(p))).reshape(shape)
+
+
+def salt_of(name: str) -> int:
+    """Call-site id (same formula as the product's kernels.salt_of; checked by the tests)."""
+    import zlib
+
+    b = name.encode()
+    return (zlib.crc32(b) << 32) | zlib.crc32(b[::-1] + b"mmfd")
+
+
+def make_drop(seed: int, p: float, dtype=None):
+    """`drop(site, x)` callback for the oracle: applies exactly the HIP kernels' mask."""
+    import torch
+
+    def drop(site, x):
+        keep = torch.from_numpy(keep_mask(seed, salt_of(site), tuple(x.shape), p))
+        return x * keep.to(x.dtype) / (1.0 - p)
+
+    return drop

@@ -1,0 +1,81 @@
+"""CPU-only checks of the drop-in API surface and of the C-ABI library (loads, exports every
+symbol include/mmfd.h declares; host-side hash matches the oracle). No GPU compute here."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import mmfd
+from mmfd import kernels as K
+from mmfd.model import MisinformationDetectionModel
+from oracle.dropout_hash import dropout_hash, salt_of
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "tests", "golden")
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "mmfd.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\*]+\s+\**(mmfd_\w+)\(", src, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = K.load()
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in K.SIGNATURES, f"{s} declared in include/mmfd.h but not bound in kernels.py"
+    assert lib.mmfd_version() >= 1
+
+
+def test_host_hash_matches_oracle():
+    for seed, salt, idx in [(0, 0, 0), (1234, salt_of("x"), 17), (2 ** 40 + 5, 2 ** 63 + 11, 2 ** 35 + 3)]:
+        assert K.dropout_hash(seed, salt, idx) == int(dropout_hash(seed, salt, np.array([idx], dtype=np.uint64))[0])
+    assert K.salt_of("representation.text.self.attn") == salt_of("representation.text.self.attn")
+
+
+def test_error_reporting_without_gpu_compute():
+    # invalid arguments are rejected on the host before any launch
+    a = K.GemmArgs()
+    a.dtype = 7
+    rc = K.lib().mmfd_gemm(a, None)
+    assert rc != 0 and b"dtype" in K.lib().mmfd_last_error_string()
+
+
+@pytest.mark.parametrize("kw,fixture_key", [({}, "param_names"), ({"factify": True, "num_classes": 5}, "factify_param_names"),
+                                             ({"text_only": True}, "text_only_param_names")])
+def test_state_dict_names_match_reference(kw, fixture_key):
+    z = np.load(os.path.join(G, "fusion_small.npz"), allow_pickle=False)
+    ref = json.loads(str(z[fixture_key]))
+    m = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, dropout=0.0,
+                                     hidden_dim=16, **kw)
+    ours = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert ours == ref
+
+
+def test_full_dims_state_dict():
+    z = np.load(os.path.join(G, "fusion_full.npz"), allow_pickle=False)
+    ref = [(a, list(b)) for a, b in json.loads(str(z["param_names"]))]
+    m = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768)
+    ours = [(k, list(v.shape)) for k, v in m.state_dict().items()]
+    assert ours == ref and len(ours) == 108
+    assert sum(p.numel() for p in m.parameters()) == 4410892
+
+
+def test_reference_checkpoint_loads():
+    """A reference `model_state_dict` (fixture: post-step params of the reference's train_epoch) loads."""
+    z = np.load(os.path.join(G, "fusion_small.npz"), allow_pickle=False)
+    sd = {k[5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("post/")}
+    m = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, dropout=0.0,
+                                     hidden_dim=16)
+    m.load_state_dict(sd)
+
+
+def test_forward_on_cpu_fails_loudly():
+    m = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, hidden_dim=16)
+    with pytest.raises(RuntimeError):
+        m(torch.randn(1, 3, 48), torch.randn(1, 3, 40), torch.randn(1, 3, 48), torch.randn(1, 3, 40))
