@@ -1,0 +1,144 @@
+"""Benchmark: claim-evidence pairs/sec of the full fine-tune training step (BASELINE config 3:
+bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 per GPU, 128 tokens,
+224x224 images, synthetic data already resident in HBM), data parallel over N GPUs (one process per
+GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
+                  [--mode finetune|frozen] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "claim–evidence pairs/sec (fwd+bwd) at bs=256; 1/2/4/8 MI355X scaling"
+GFLOP_PER_PAIR = {"finetune": 351.18, "frozen": 121.11}  # BASELINE.md §3 (FlopCounterMode, fwd+bwd)
+PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(steps=2, batch=4):
+    """The oracle's CPU restatement of the same step, timed on this host (bounded sample)."""
+    from oracle.fusion_head import init_params_like_reference
+    from oracle.train_step import BERT_BASE, VIT_B16, OracleTrainer, bert_names, vit_names
+    from mmfd.dataset import synthetic_batch
+    from mmfd.model import MisinformationDetectionModel
+
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    head_names = [(k, list(v.shape)) for k, v in MisinformationDetectionModel(768, 768).state_dict().items()]
+    tr = OracleTrainer(init_params_like_reference(bert_names(BERT_BASE), 1),
+                       init_params_like_reference(vit_names(VIT_B16), 2),
+                       init_params_like_reference(head_names, 3))
+    b = synthetic_batch(batch, device="cpu", seed=7)
+    tr.step(b)  # warmup
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(b)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(batch / dt, 4), "unit": "pairs/s", "cores": cores, "kind": "port",
+            "sample": f"oracle CPU restatement (fp32 torch CPU) of the same full fine-tune step at bs={batch}, "
+                      f"1 warmup + {steps} timed steps, {dt:.2f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dp = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        from mmfd.dp import GradAllReduce
+        dp = GradAllReduce()
+
+    import mmfd
+    from mmfd import kernels as K
+    from mmfd.dataset import synthetic_batch
+    from mmfd.train import build_flagship
+
+    K.load()
+    tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
+    batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
+
+    for _ in range(args.warmup):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    probe = K.GemmProbe()
+    t0 = time.perf_counter()
+    with probe:
+        for _ in range(args.steps):
+            loss = tr.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    ms = 1000.0 * elapsed / args.steps
+    pairs = args.batch * world * args.steps / elapsed
+    loss_val = loss[0].item()
+
+    prof = probe.summary()
+    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    dom_name, d = dom
+    achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+    gemm_ms = sum(v["ms"] for v in prof.values()) / args.steps
+    gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
+
+    if rank == 0:
+        step_tflops = pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3
+        out = {
+            "metric": METRIC, "value": round(pairs, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.precision, "data": "synthetic (Factify-shaped pairs, random-init weights)",
+            "config": {"workload": ("full fine-tune " if args.mode == "finetune" else "frozen-encoder ") +
+                       "bert-base-uncased + ViT-B/16 + fusion head (768/768, E=256, H=8), fwd+bwd+AdamW",
+                       "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                         "launches_per_step": d["launches"] // args.steps,
+                         "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
+                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])},
+            "step_tflops_per_gpu": round(step_tflops, 1),
+            "step_mfma_frac": round(step_tflops / peak, 4),
+            "gemm_ms_per_step": round(gemm_ms, 2), "gemm_tflops_all_shapes": round(gemm_tf, 1),
+            "final_loss": round(loss_val, 4),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline()
+            except Exception as e:  # the baseline must never hide the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

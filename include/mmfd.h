@@ -152,9 +152,10 @@ int mmfd_seq_mean_bwd(int dtype, int64_t B, int64_t L, int64_t D, const void* do
 
 /* ------------------------------------------------------------------------------------------- */
 /* Summed per-path cross entropy (train.py:165-169: sum_i CrossEntropyLoss(y_i, labels[:, i])).  */
-/* logits: n_paths pointers (device array of device pointers) each [B][C] fp32; labels int64    */
+/* logits: HOST array of n_paths device pointers, each [B][C] fp32; labels int64 (device)      */
 /* [B][label_ld] with path i in column i. loss[0] = total, loss[1+i] = path i (mean over B).     */
-/* dlogits (optional, n_paths pointers) receive d(total)/d(logits) * (*dloss_scale or 1).        */
+/* dlogits (optional host array of n_paths device pointers) receive d(total)/d(logits) *        */
+/* (*dloss_scale or 1), dloss_scale being a device scalar (NULL = 1).                            */
 /* ------------------------------------------------------------------------------------------- */
 int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits,
                       const int64_t* labels, int64_t label_ld, float* loss, float* const* dlogits,

@@ -36,16 +36,21 @@ __global__ void seq_mean_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __
 // ---------------------------------------------------------------------------------------------
 // summed cross entropy over paths; one block, rows = n_paths * B
 // ---------------------------------------------------------------------------------------------
-__global__ void xent_kernel(int n_paths, int64_t B, int64_t C, const float* const* __restrict__ logits,
-                            const int64_t* __restrict__ labels, int64_t label_ld, float* __restrict__ loss,
-                            float* const* __restrict__ dlogits, const float* __restrict__ dscale) {
+struct XentPtrs {
+  const float* logits[4];
+  float* dlogits[4];
+  int has_grad;
+};
+
+__global__ void xent_kernel(int n_paths, int64_t B, int64_t C, XentPtrs ptrs, const int64_t* __restrict__ labels,
+                            int64_t label_ld, float* __restrict__ loss, const float* __restrict__ dscale) {
   __shared__ float red[4][256];
   const float sc = dscale ? *dscale : 1.0f;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
   for (int64_t rr = threadIdx.x; rr < (int64_t)n_paths * B; rr += blockDim.x) {
     const int path = (int)(rr / B);
     const int64_t b = rr % B;
-    const float* z = logits[path] + b * C;
+    const float* z = ptrs.logits[path] + b * C;
     float mx = -INFINITY;
     for (int64_t c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
     float se = 0.f;
@@ -53,8 +58,8 @@ __global__ void xent_kernel(int n_paths, int64_t B, int64_t C, const float* cons
     const float lse = mx + logf(se);
     const int64_t y = labels[b * label_ld + path];
     part[path] += lse - z[y];
-    if (dlogits) {
-      float* dz = dlogits[path] + b * C;
+    if (ptrs.has_grad) {
+      float* dz = ptrs.dlogits[path] + b * C;
       for (int64_t c = 0; c < C; ++c) dz[c] = (expf(z[c] - lse) - (c == y ? 1.f : 0.f)) * sc / (float)B;
     }
   }
@@ -277,9 +282,15 @@ extern "C" int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float*
                                  int64_t label_ld, float* loss, float* const* dlogits, const float* dloss_scale,
                                  mmfd_stream_t stream) {
   MMFD_CHECK_ARG(n_paths >= 1 && n_paths <= 4, "xent: 1..4 paths");
-  MMFD_CHECK_ARG(B > 0 && C > 0, "xent: bad shape");
-  hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_paths, B, C, logits, labels, label_ld, loss,
-                     dlogits, dloss_scale);
+  MMFD_CHECK_ARG(B > 0 && C > 0 && logits, "xent: bad shape");
+  XentPtrs ptrs = {};
+  for (int i = 0; i < n_paths; ++i) {
+    ptrs.logits[i] = logits[i];
+    ptrs.dlogits[i] = dlogits ? dlogits[i] : nullptr;
+  }
+  ptrs.has_grad = dlogits != nullptr;
+  hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_paths, B, C, ptrs, labels, label_ld, loss,
+                     dloss_scale);
   MMFD_CHECK_LAUNCH("xent");
   return 0;
 }

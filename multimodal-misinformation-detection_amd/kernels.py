@@ -210,6 +210,43 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
+_PROBE = None
+
+
+class GemmProbe:
+    """Records HIP events around every MFMA-path GEMM launch while active (bench.py roofline):
+    per kernel instantiation, the algorithmic FLOPs (2*M*N*K) and the launch's device time."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROBE
+        _PROBE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _PROBE
+        _PROBE = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for key, flops, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            d = out.setdefault(key, {"launches": 0, "flops": 0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["ms"] += ms
+        return out
+
+
+def _kernel_name(a, split):
+    t = {F32: "float", BF16: "__bf16"}
+    base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
+    return base + (" (split-K)" if split else "")
+
+
 def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
          residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0):
     """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
@@ -262,7 +299,16 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
     if need > 0:
         ws = torch.empty(need // 4 + 1, device=A.device, dtype=torch.float32)
         a.workspace, a.workspace_bytes = ws.data_ptr(), need
+    probe = _PROBE
+    rec = probe is not None and M >= 16 and N >= 16 and K >= 16
+    if rec:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     _check(L.mmfd_gemm(ctypes.byref(a), _stream()), "mmfd_gemm")
+    if rec:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        probe.records.append((_kernel_name(a, need > 0), 2 * M * N * K, e0, e1))
     return out
 
 
@@ -407,18 +453,6 @@ def seq_mean_bwd(dout, L, dx=None):
     return dx
 
 
-class _PtrArray:
-    """A small device array of device pointers (kept alive with its tensors)."""
-
-    def __init__(self, tensors, device):
-        self.tensors = list(tensors)
-        host = torch.tensor([t.data_ptr() for t in self.tensors], dtype=torch.int64)
-        self.dev = host.to(device, non_blocking=False)
-
-    def ptr(self):
-        return _ptr(self.dev)
-
-
 def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None):
     """logits: list of [B, C] fp32 tensors (paths), labels: int64 [B, n_paths (or more)].
     Returns (loss [1 + n_paths] fp32 device tensor, list of dlogits or None)."""
@@ -428,12 +462,11 @@ def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None):
     logits = [l.contiguous().float() for l in logits]
     labels = labels.contiguous()
     loss = torch.empty(1 + n, device=dev, dtype=torch.float32)
-    lp = _PtrArray(logits, dev)
+    lp = (ctypes.c_void_p * n)(*[l.data_ptr() for l in logits])
     dl = [torch.empty_like(l) for l in logits] if want_grad else None
-    dp = _PtrArray(dl, dev) if want_grad else None
-    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp.ptr(), _ptr(labels), labels.stride(0), _ptr(loss),
-                                   dp.ptr() if dp is not None else None, _ptr(dloss_scale), _stream()),
-           "mmfd_xent_fwd_bwd")
+    dp = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dl]) if want_grad else None
+    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp, _ptr(labels), labels.stride(0), _ptr(loss), dp, _ptr(dloss_scale),
+                                   _stream()), "mmfd_xent_fwd_bwd")
     return loss, dl
 
 
