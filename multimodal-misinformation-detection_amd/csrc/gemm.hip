@@ -70,22 +70,40 @@ struct Stage {
 
   __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int64_t mn0, int64_t mn_ext,
                                        int64_t k0, int64_t K, int tid) {
+    // Interior tiles (the common case, a block-uniform test) load with no predication at all, so
+    // the loads stay in flight across the MFMAs of the current tile. Edge tiles load from clamped
+    // (always valid) addresses and zero the out-of-range chunks with a select.
+    const bool interior = (LAYOUT == 0) ? (mn0 + 128 <= mn_ext && k0 + GT<T>::BK <= K)
+                                        : (k0 + GT<T>::BK <= K && mn0 + 128 <= mn_ext);
+    if (interior) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + NT * i;
+        int64_t row, col;
+        if (LAYOUT == 0) { row = mn0 + (c >> 3); col = k0 + (int64_t)(c & 7) * GT<T>::EPC; }
+        else { row = k0 + c / GT<T>::MN_CPR; col = mn0 + (int64_t)(c % GT<T>::MN_CPR) * GT<T>::EPC; }
+        r[i] = *reinterpret_cast<const uint4*>(p + row * ld + col);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = tid + NT * i;
-      int64_t row, col;  // row index in the stored matrix, column (elements)
-      bool ok;
+      int64_t row, col, rmax, cmax;
       if (LAYOUT == 0) {
         const int tr = c >> 3, kc = c & 7;
         row = mn0 + tr; col = k0 + (int64_t)kc * GT<T>::EPC;
-        ok = (row < mn_ext) && (col < K);
+        rmax = mn_ext; cmax = K;
       } else {
         const int tr = c / GT<T>::MN_CPR, cc = c % GT<T>::MN_CPR;
         row = k0 + tr; col = mn0 + (int64_t)cc * GT<T>::EPC;
-        ok = (row < K) && (col < mn_ext);
+        rmax = K; cmax = mn_ext;
       }
-      if (ok) r[i] = *reinterpret_cast<const uint4*>(p + row * ld + col);
-      else r[i] = make_uint4(0, 0, 0, 0);
+      const bool ok = (row < rmax) && (col < cmax);
+      const int64_t rr = row < rmax ? row : rmax - 1;
+      const int64_t cc2 = col < cmax ? col : cmax - GT<T>::EPC;
+      const uint4 v = *reinterpret_cast<const uint4*>(p + rr * ld + cc2);
+      r[i].x = ok ? v.x : 0u; r[i].y = ok ? v.y : 0u; r[i].z = ok ? v.z : 0u; r[i].w = ok ? v.w : 0u;
     }
   }
 
@@ -208,34 +226,44 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 
 #undef LDS_A
 #undef LDS_B
+  // ---- epilogue: stage the 128x128 fp32 tile through LDS in two 64-row halves, then every thread
+  // handles 4 consecutive columns of a row (coalesced 8/16-B stores, uniform epilogue code). Static
+  // accumulator indexing only, so the accumulators never leave registers.
+  constexpr int LDC = BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
-  if (ws) {
-    float* slab = ws + (int64_t)blockIdx.z * M * N;
+  const uint64_t seed = (!ws && e.p > 0.0f) ? *e.seed : 0ull;
+  float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t col = n0 + wn * 64 + j * 16 + ci;
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = m0 + wm * 64 + i * 16 + 4 * g + r;
-          if (row < M && col < N) slab[row * N + col] = alpha * acc[i][j][r];
-        }
-      }
-    return;
-  }
-  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+          for (int r = 0; r < 4; ++r) ct[(i * 16 + 4 * g + r) * LDC + wn * 64 + j * 16 + ci] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 64 * (BN / 4); idx += NT) {
+      const int lr = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+      const int64_t row = m0 + half * 64 + lr;
+      const int64_t col = n0 + c4;
+      if (row >= M || col >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(ct + lr * LDC + c4);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      if (slab) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 16 + ci;
+        for (int q = 0; q < 4; ++q)
+          if (col + q < N) slab[row * N + col + q] = alpha * vv[q];
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + 4 * g + r;
-        if (row < M && col < N) epilogue_store<TC>(e, C, ldc, N, row, col, alpha * acc[i][j][r], seed);
+        for (int q = 0; q < 4; ++q)
+          if (col + q < N) epilogue_store<TC>(e, C, ldc, N, row, col + q, alpha * vv[q], seed);
       }
     }
+    __syncthreads();
+  }
 }
 
 template <typename TC>
