@@ -129,6 +129,10 @@ __device__ __forceinline__ uint2 lds_read_tr16(const char* addr) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// shared deterministic reduction of per-block column partials (gemm.hip)
+__global__ void mmfd_reduce_partials_kernel(const float* __restrict__ part, int nparts, int64_t stride, int64_t N,
+                                            float* __restrict__ out, float beta);
+
 __device__ __forceinline__ int xcd_remap(int id, int total) {
   // blocks are dealt round-robin over the 8 XCDs; give each XCD a contiguous run of tiles
   // (bijective for any total, speed only).

@@ -16,16 +16,17 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, ROWB = 128, NT = 256;
-constexpr int TILE_BYTES = 16384;  // one operand tile, any layout / dtype
+// Tile geometry: 256 (M) x 128 (N) x 128 B of K (64 bf16 / 32 fp32), 8 waves as 4 (M) x 2 (N), each
+// wave a 64 x 64 block of 4 x 4 16x16 MFMA tiles. Three LDS stages of 48 KB (A 32 KB + B 16 KB).
+constexpr int BM = 256, BN = 128, ROWB = 128, NT = 512, NWAVES = 8;
+constexpr int A_BYTES = 32768, B_BYTES = 16384, STAGE_BYTES = A_BYTES + B_BYTES, NSTAGE = 3;
+constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;  // 147456
 
 template <typename T> struct GT {
   static constexpr int ESZ = sizeof(T);
-  static constexpr int BK = ROWB / ESZ;      // K per tile
-  static constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
-  static constexpr int KCH = BK / Mma<T>::KC; // MFMA chunks per tile (2)
-  static constexpr int MN_ROWB = 128 * ESZ;  // bytes per k-row of an MN-contiguous image
-  static constexpr int MN_CPR = MN_ROWB / 16;
+  static constexpr int BK = ROWB / ESZ;        // K per tile
+  static constexpr int EPC = 16 / ESZ;         // elements per 16-B chunk
+  static constexpr int KCH = BK / Mma<T>::KC;  // MFMA chunks per tile (2)
 };
 
 struct EpiArgs {
@@ -60,115 +61,123 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
   *cp = from_f32<TC>(z);
 }
 
-// --------------------------------------------------------------------------------------------
-// operand staging
-// --------------------------------------------------------------------------------------------
-template <typename T, int LAYOUT>
-struct Stage {
-  // 4 x 16-byte chunks per thread per tile
-  uint4 r[4];
+// -------------------------------------------------------------------------------------------------
+// LDS images. Operand layout 0 ("K-contiguous": A[m][k] / nn.Linear W[n][k]): [rows][128 B], 16-B
+// chunk c of row r at chunk c ^ (r & 7) (conflict-free ds_read_b128 fragments). Layout 1
+// ("MN-contiguous": A[k][m] / B[k][n]): [BK rows][MNW elements]; bf16 fragments come from
+// ds_read_b64_tr_b16 with 8-B unit u of row r at u ^ 4*((r&3) | ((r>>3)&1)<<2) (conflict-free tr
+// reads), fp32 fragments from 4 ds_read_b32 with chunk c at c ^ 4*((r>>2)&1).
+// -------------------------------------------------------------------------------------------------
+template <typename T, int LAYOUT, int MNW>
+struct Img {
+  static constexpr int RBY = LAYOUT == 0 ? ROWB : MNW * (int)sizeof(T);  // bytes per image row
+  static constexpr int CPR = RBY / 16;                                    // 16-B chunks per row
+  static constexpr int RPI = 1024 / RBY;                                  // rows per 1-KB DMA piece
+  __device__ __forceinline__ static int swz(int r, int c) {  // physical chunk <-> logical chunk
+    if (LAYOUT == 0) return c ^ (r & 7);
+    if (sizeof(T) == 2) return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
+    return c ^ (4 * ((r >> 2) & 1));
+  }
+};
 
-  __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int64_t mn0, int64_t mn_ext,
-                                       int64_t k0, int64_t K, int tid) {
-    // Interior tiles (the common case, a block-uniform test) load with no predication at all, so
-    // the loads stay in flight across the MFMAs of the current tile. Edge tiles load from clamped
-    // (always valid) addresses and zero the out-of-range chunks with a select.
-    const bool interior = (LAYOUT == 0) ? (mn0 + 128 <= mn_ext && k0 + GT<T>::BK <= K)
-                                        : (k0 + GT<T>::BK <= K && mn0 + 128 <= mn_ext);
-    if (interior) {
+constexpr uint32_t OOB = 0x80000000u;  // operands are < 2 GB (checked on the host)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// One 1-KB LDS-DMA piece: lane l's 16 bytes land at lds_dst + 16 l. Written as inline asm so that
+// hipcc does not treat later ds_reads as dependent on it (it would drain vmcnt(0) before every
+// k-step); completion is tracked by hand with counted s_waitcnt vmcnt + s_barrier.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, uint32_t voff, uint32_t soff) {
+  const uint32_t lds = (uint32_t)(size_t)(MMFD_LDS char*)lds_dst;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(voff), "s"(rs), "s"(soff)
+      : "memory");
+}
+
+// One operand's share of a stage fill: NP 1-KB LDS-DMA pieces per wave (buffer_load ... lds). The
+// per-lane source offsets are loop invariant (the K tile advances through soffset) and chunks
+// outside the matrix point past num_records, so the DMA writes zeros there.
+template <typename T, int LAYOUT, int MNW, int NP>
+struct Fill {
+  uint32_t off[NP];
+  __device__ __forceinline__ void init(int64_t ld, int64_t mn0, int64_t mn_ext, int wave, int lane) {
+    using I = Img<T, LAYOUT, MNW>;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + NT * i;
-        int64_t row, col;
-        if (LAYOUT == 0) { row = mn0 + (c >> 3); col = k0 + (int64_t)(c & 7) * GT<T>::EPC; }
-        else { row = k0 + c / GT<T>::MN_CPR; col = mn0 + (int64_t)(c % GT<T>::MN_CPR) * GT<T>::EPC; }
-        r[i] = *reinterpret_cast<const uint4*>(p + row * ld + col);
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      int64_t row, col, rmax, cmax;
-      if (LAYOUT == 0) {
-        const int tr = c >> 3, kc = c & 7;
-        row = mn0 + tr; col = k0 + (int64_t)kc * GT<T>::EPC;
-        rmax = mn_ext; cmax = K;
-      } else {
-        const int tr = c / GT<T>::MN_CPR, cc = c % GT<T>::MN_CPR;
-        row = k0 + tr; col = mn0 + (int64_t)cc * GT<T>::EPC;
-        rmax = K; cmax = mn_ext;
-      }
-      const bool ok = (row < rmax) && (col < cmax);
-      const int64_t rr = row < rmax ? row : rmax - 1;
-      const int64_t cc2 = col < cmax ? col : cmax - GT<T>::EPC;
-      const uint4 v = *reinterpret_cast<const uint4*>(p + rr * ld + cc2);
-      r[i].x = ok ? v.x : 0u; r[i].y = ok ? v.y : 0u; r[i].z = ok ? v.z : 0u; r[i].w = ok ? v.w : 0u;
+    for (int j = 0; j < NP; ++j) {
+      const int q = wave * NP + j;                     // piece index within the image
+      const int row = q * I::RPI + lane / I::CPR;      // image row this lane writes
+      const int c = I::swz(row, lane % I::CPR);        // source chunk for that position
+      int64_t el;
+      bool ok;
+      if (LAYOUT == 0) { el = (mn0 + row) * ld + (int64_t)c * GT<T>::EPC; ok = mn0 + row < mn_ext; }
+      else { el = (int64_t)row * ld + mn0 + (int64_t)c * GT<T>::EPC; ok = mn0 + (int64_t)c * GT<T>::EPC < mn_ext; }
+      off[j] = ok ? (uint32_t)(el * (int64_t)sizeof(T)) : OOB;
     }
   }
-
-  __device__ __forceinline__ void store(char* lds, int tid) const {
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, uint32_t soff, bool tail, int64_t k0,
+                                        int64_t K, int wave, int lane) {
+    using I = Img<T, LAYOUT, MNW>;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      int off;
-      if (LAYOUT == 0) {
-        const int tr = c >> 3, kc = c & 7;
-        off = tr * ROWB + ((kc ^ (tr & 7)) << 4);
-      } else {
-        const int tr = c / GT<T>::MN_CPR, cc = c % GT<T>::MN_CPR;
-        int sc;
-        if (sizeof(T) == 2) sc = cc ^ (2 * ((tr & 3) | (((tr >> 3) & 1) << 2)));
-        else sc = cc ^ (4 * ((tr >> 2) & 1));
-        off = tr * GT<T>::MN_ROWB + (sc << 4);
+    for (int j = 0; j < NP; ++j) {
+      uint32_t o = off[j];
+      if (LAYOUT == 0 && tail) {  // partial last K tile: zero the chunks past K
+        const int row = (wave * NP + j) * I::RPI + lane / I::CPR;
+        const int c = I::swz(row, lane % I::CPR);
+        if (k0 + (int64_t)c * GT<T>::EPC >= K) o = OOB;
       }
-      *reinterpret_cast<uint4*>(lds + off) = r[i];
+      dma16(rs, img + (wave * NP + j) * 1024, o, soff);
     }
   }
 };
 
-// fragment of 16 rows (K-contig) / 16 columns (MN-contig) for MFMA chunk kc
-template <typename T, int LAYOUT>
-__device__ __forceinline__ uint4 load_frag(const char* lds, int sub, int kc, int lane) {
+// 16-row (layout 0) / 16-column (layout 1) MFMA fragment for K chunk kc
+template <typename T, int LAYOUT, int MNW>
+__device__ __forceinline__ uint4 load_frag(const char* img, int sub, int kc, int lane) {
+  using I = Img<T, LAYOUT, MNW>;
   const int g = lane >> 4, i = lane & 15;
   if (LAYOUT == 0) {
     const int row = sub * 16 + i;
-    const int c = kc * 4 + g;
-    return lds_read16(lds, row * ROWB + ((c ^ (row & 7)) << 4));
+    return lds_read16(img, row * ROWB + (I::swz(row, kc * 4 + g) << 4));
   } else if (sizeof(T) == 2) {
     const int q = i >> 2, p = i & 3;
     const int r1 = kc * 32 + 8 * g + q, r2 = r1 + 4;
-    const int u = sub * 4 + p;
-    const int f1 = 4 * ((r1 & 3) | (((r1 >> 3) & 1) << 2));
-    const int f2 = 4 * ((r2 & 3) | (((r2 >> 3) & 1) << 2));
-    const uint2 a = lds_read_tr16(lds + r1 * 256 + ((u ^ f1) << 3));
-    const uint2 b = lds_read_tr16(lds + r2 * 256 + ((u ^ f2) << 3));
+    const int u = sub * 4 + p;  // 8-B unit (4 bf16)
+    const uint2 a = lds_read_tr16(img + r1 * I::RBY + (I::swz(r1, u >> 1) << 4) + ((u & 1) << 3));
+    const uint2 b = lds_read_tr16(img + r2 * I::RBY + (I::swz(r2, u >> 1) << 4) + ((u & 1) << 3));
     return make_uint4(a.x, a.y, b.x, b.y);
   } else {
     const int col = sub * 16 + i;
-    const int ch = col >> 2, w = (col & 3) * 4;
     uint32_t v[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int row = kc * 16 + 4 * g + s;
-      const int sc = ch ^ (4 * ((row >> 2) & 1));
-      v[s] = *reinterpret_cast<const uint32_t*>(lds + row * 512 + (sc << 4) + w);
+      v[s] = *reinterpret_cast<const uint32_t*>(img + row * I::RBY + (I::swz(row, col >> 2) << 4) + (col & 3) * 4);
     }
     return make_uint4(v[0], v[1], v[2], v[3]);
   }
 }
 
 template <typename T, int TA, int TB, typename TC>
-__global__ void __launch_bounds__(NT, 2)
+__global__ void __launch_bounds__(NT, 1)
 gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                  TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
                  int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // buffer b: A image at smem + 2*b*TILE_BYTES, B image right after it
-#define LDS_A(b) (smem + (b) * 2 * TILE_BYTES)
-#define LDS_B(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
+  constexpr int APIECES = A_BYTES / 1024 / NWAVES;  // 4 pieces per wave
+  constexpr int BPIECES = B_BYTES / 1024 / NWAVES;  // 2 pieces per wave
+  constexpr int PIECES = APIECES + BPIECES;         // DMA instructions per wave per tile
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int gx = gridDim.x, gy = gridDim.y;
   const int lin = blockIdx.y * gx + blockIdx.x;
@@ -178,7 +187,7 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 
   const int nkt_total = (int)((K + GT<T>::BK - 1) / GT<T>::BK);
   const int kt0 = blockIdx.z * tiles_per_split;
-  const int kt1 = min(nkt_total, kt0 + tiles_per_split);
+  const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -186,57 +195,59 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage<T, TA> sa;
-  Stage<T, TB> sb;
-  if (kt0 < kt1) {
-    sa.load(A, lda, m0, M, (int64_t)kt0 * GT<T>::BK, K, tid);
-    sb.load(B, ldb, n0, N, (int64_t)kt0 * GT<T>::BK, K, tid);
-    sa.store(LDS_A(0), tid);
-    sb.store(LDS_B(0), tid);
-  }
-  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * (int64_t)sizeof(T));
+  Fill<T, TA, BM, APIECES> fa;
+  Fill<T, TB, BN, BPIECES> fb;
+  fa.init(lda, m0, M, wave, lane);
+  fb.init(ldb, n0, N, wave, lane);
 
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = (kt + 1) < kt1;
-    if (more) {
-      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * GT<T>::BK, K, tid);
-      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * GT<T>::BK, K, tid);
-    }
-    const char* la = LDS_A(cur);
-    const char* lb = LDS_B(cur);
+  auto issue = [&](int t) {
+    const int64_t k0 = (int64_t)(kt0 + t) * GT<T>::BK;
+    const bool tail = k0 + GT<T>::BK > K;
+    char* st = smem + (t % NSTAGE) * STAGE_BYTES;
+    fa.issue(rsa, st, (uint32_t)(k0 * (TA == 0 ? 1 : lda) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
+    fb.issue(rsb, st + A_BYTES, (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
+  };
+
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed (keep tile t+1 in flight); the barrier also retires every wave's reads of the
+    // stage about to be refilled (tile t-1)
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) issue(t + 2);
+    const char* la = smem + (t % NSTAGE) * STAGE_BYTES;
+    const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kc = 0; kc < GT<T>::KCH; ++kc) {
-      uint4 fa[4], fb[4];
+      uint4 xa[4], xb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = load_frag<T, TA>(la, wm * 4 + i, kc, lane);
+      for (int i = 0; i < 4; ++i) xa[i] = load_frag<T, TA, BM>(la, wm * 4 + i, kc, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = load_frag<T, TB>(lb, wn * 4 + j, kc, lane);
+      for (int j = 0; j < 4; ++j) xb[j] = load_frag<T, TB, BN>(lb, wn * 4 + j, kc, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+        for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], xa[i], xb[j]);
     }
-    if (more) {
-      sa.store(LDS_A(cur ^ 1), tid);
-      sb.store(LDS_B(cur ^ 1), tid);
-    }
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-#undef LDS_A
-#undef LDS_B
-  // ---- epilogue: stage the 128x128 fp32 tile through LDS in two 64-row halves, then every thread
-  // handles 4 consecutive columns of a row (coalesced 8/16-B stores, uniform epilogue code). Static
-  // accumulator indexing only, so the accumulators never leave registers.
+  // ---- epilogue: stage the 256x128 fp32 tile through LDS in four 64-row quarters (one wave row
+  // each), then every thread handles 4 consecutive columns of a row (coalesced stores).
   constexpr int LDC = BN + 4;
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
   const uint64_t seed = (!ws && e.p > 0.0f) ? *e.seed : 0ull;
   float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wm == half) {
+  for (int qtr = 0; qtr < 4; ++qtr) {
+    if (wm == qtr) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -247,7 +258,7 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
     __syncthreads();
     for (int idx = tid; idx < 64 * (BN / 4); idx += NT) {
       const int lr = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
-      const int64_t row = m0 + half * 64 + lr;
+      const int64_t row = m0 + qtr * 64 + lr;
       const int64_t col = n0 + c4;
       if (row >= M || col >= N) continue;
       const float4 v = *reinterpret_cast<const float4*>(ct + lr * LDC + c4);
@@ -303,7 +314,12 @@ template <typename T, int TA, int TB, typename TC>
 void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps,
                  hipStream_t s) {
   dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
-  hipLaunchKernelGGL((gemm_mfma_kernel<T, TA, TB, TC>), grid, dim3(NT), 4 * TILE_BYTES, s,
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mfma_kernel<T, TA, TB, TC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_mfma_kernel<T, TA, TB, TC>), grid, dim3(NT), LDS_BYTES, s,
                      (const T*)a.A, a.lda, (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K,
                      a.alpha, tps, e);
 }
@@ -326,6 +342,9 @@ bool mfma_ok(const mmfd_gemm_args& a) {
   const int64_t b_ext = a.trans_b ? a.N : a.K;
   if (a_ext % epc || b_ext % epc) return false;
   if (a.M < 16 || a.N < 16 || a.K < 16) return false;
+  const int64_t esz = a.dtype == MMFD_BF16 ? 2 : 4;
+  const int64_t abytes = (a.trans_a ? a.K : a.M) * a.lda * esz, bbytes = (a.trans_b ? a.K : a.N) * a.ldb * esz;
+  if (abytes >= (1ll << 31) - 4096 || bbytes >= (1ll << 31) - 4096) return false;  // 32-bit buffer offsets
   return true;
 }
 
@@ -335,8 +354,8 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
   const int64_t nkt = (a.K + T - 1) / T;
   int splits = 1;
   if (a.splits > 0) splits = a.splits;
-  else if (tiles < 240 && nkt >= 16) {
-    splits = (int)((512 + tiles - 1) / tiles);
+  else if (tiles < 200 && nkt >= 16) {
+    splits = (int)((384 + tiles - 1) / tiles);
     splits = (int)std::min<int64_t>(splits, nkt / 8);
     splits = std::min(splits, 16);
     if (splits < 1) splits = 1;
@@ -426,6 +445,37 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
 // column sums (bias gradients), deterministic two-pass
 // ------------------------------------------------------------------------------------------------
 namespace {
+// pass 1 (vector path): block = 4 waves x 64 lanes; a lane owns one 16-B chunk of columns, the 4
+// waves stride over the block's row slab; the waves' partials are combined in LDS.
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_partial_vec_kernel(const T* __restrict__ X, int64_t ldx, int64_t M,
+                                                                 int64_t N, int64_t rows_per_block,
+                                                                 float* __restrict__ part) {
+  constexpr int EPC = 16 / sizeof(T);
+  __shared__ float red[4][64 * EPC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = ((int64_t)blockIdx.x * 64 + lane) * EPC;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float acc[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) acc[e] = 0.f;
+  if (col < N) {
+    for (int64_t r = r0 + wave; r < r1; r += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(X + r * ldx + col);
+      const T* t = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) acc[e] += to_f32(t[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) red[wave][lane * EPC + e] = acc[e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * EPC; i += 256) {
+    const int64_t c = (int64_t)blockIdx.x * 64 * EPC + i;
+    if (c < N) part[(int64_t)blockIdx.y * N + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
 template <typename T>
 __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int64_t N,
                                       int64_t rows_per_block, float* __restrict__ part) {
@@ -437,15 +487,26 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ldx, int6
   for (int64_t r = r0; r < r1; ++r) s += to_f32(X[r * ldx + col]);
   part[(int64_t)blockIdx.y * N + col] = s;
 }
-__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int64_t N,
-                                    float* __restrict__ out, float beta) {
-  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * N + col];
-  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + s;
-}
 }  // namespace
+
+// pass 2, shared with the LayerNorm backward: out[c] = beta*out[c] + sum_p part[p*stride + c];
+// block = 64 columns x 4 waves splitting the partials, combined through LDS.
+__global__ void __launch_bounds__(256) mmfd_reduce_partials_kernel(const float* __restrict__ part, int nparts,
+                                                                   int64_t stride, int64_t N, float* __restrict__ out,
+                                                                   float beta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < N)
+    for (int p = wave; p < nparts; p += 4) s += part[(int64_t)p * stride + col];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && col < N) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
+  }
+}
 
 extern "C" int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, float* out,
                            float beta, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
@@ -456,13 +517,23 @@ extern "C" int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64
   if (workspace_bytes < (int64_t)nparts * N * 4) nparts = (int)(workspace_bytes / (N * 4));
   MMFD_CHECK_ARG(nparts >= 1 && workspace, "mmfd_colsum: workspace too small");
   const int64_t rpb = (M + nparts - 1) / nparts;
-  dim3 g1((unsigned)((N + 255) / 256), (unsigned)nparts);
-  if (dtype == MMFD_BF16)
-    hipLaunchKernelGGL((colsum_partial_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)X, ldx, M, N, rpb, (float*)workspace);
-  else
-    hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)X, ldx, M, N, rpb, (float*)workspace);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s,
-                     (const float*)workspace, nparts, N, out, beta);
+  const int epc = dtype == MMFD_BF16 ? 8 : 4;
+  const bool vec = (N % epc) == 0 && (ldx % epc) == 0 && ((uintptr_t)X & 15) == 0;
+  if (vec) {
+    dim3 g1((unsigned)((N / epc + 63) / 64), (unsigned)nparts);
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((colsum_partial_vec_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)X, ldx, M, N, rpb, (float*)workspace);
+    else
+      hipLaunchKernelGGL((colsum_partial_vec_kernel<float>), g1, dim3(256), 0, s, (const float*)X, ldx, M, N, rpb, (float*)workspace);
+  } else {
+    dim3 g1((unsigned)((N + 255) / 256), (unsigned)nparts);
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((colsum_partial_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)X, ldx, M, N, rpb, (float*)workspace);
+    else
+      hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)X, ldx, M, N, rpb, (float*)workspace);
+  }
+  hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s,
+                     (const float*)workspace, nparts, N, N, out, beta);
   MMFD_CHECK_LAUNCH("colsum");
   return 0;
 }

@@ -163,18 +163,6 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, int width, co
   }
 }
 
-__global__ void ln_bwd_final_kernel(const float* __restrict__ part, int nparts, int width, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta, float beta_acc) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= width) return;
-  float sg = 0.f, sb = 0.f;
-  for (int b = 0; b < nparts; ++b) {
-    sg += part[((int64_t)b * 2 + 0) * width + col];
-    sb += part[((int64_t)b * 2 + 1) * width + col];
-  }
-  if (dgamma) dgamma[col] = (beta_acc != 0.f ? beta_acc * dgamma[col] : 0.f) + sg;
-  if (dbeta) dbeta[col] = (beta_acc != 0.f ? beta_acc * dbeta[col] : 0.f) + sb;
-}
 }  // namespace
 
 extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
@@ -217,9 +205,13 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
     hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const float*)dy, lddy,
                        (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx, (const float*)dx_add, ldadd,
                        (float*)dx_drop, p, thr, seed, salt, (float*)workspace);
-  if (dgamma || dbeta)
-    hipLaunchKernelGGL(ln_bwd_final_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, s, (const float*)workspace,
-                       nblocks, (int)width, dgamma, dbeta, beta_acc);
+  // part layout [block][2][width]: gamma partials at offset 0, beta partials at +width, stride 2*width
+  if (dgamma)
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(256), 0, s,
+                       (const float*)workspace, nblocks, 2 * width, width, dgamma, beta_acc);
+  if (dbeta)
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(256), 0, s,
+                       (const float*)workspace + width, nblocks, 2 * width, width, dbeta, beta_acc);
   MMFD_CHECK_LAUNCH("layernorm_bwd");
   return 0;
 }
