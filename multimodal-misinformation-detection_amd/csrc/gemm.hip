@@ -37,6 +37,7 @@ struct EpiArgs {
   float p; uint32_t thr; float keep_scale;
   const uint64_t* seed; uint64_t salt;
   float beta;
+  int vec;  // host-checked: C / residual / aux 16-B aligned with leading dims multiple of 8
 };
 
 template <typename TC>
@@ -59,6 +60,79 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
   TC* cp = C + row * ldc + col;
   if (e.beta != 0.0f) z += e.beta * to_f32(*cp);
   *cp = from_f32<TC>(z);
+}
+
+template <typename TC> struct V8;
+template <> struct V8<bf16> {
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[8]) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float (&v)[8]) {
+    bf16x8 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, o);
+  }
+};
+template <> struct V8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// 8 consecutive columns [col, col+8) of one row; same operation order as epilogue_store
+template <typename TC>
+__device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t ldc, int64_t N, int64_t row,
+                                                int64_t col, float (&z)[8], uint64_t seed) {
+  if (e.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col), b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
+    z[0] += b0.x; z[1] += b0.y; z[2] += b0.z; z[3] += b0.w; z[4] += b1.x; z[5] += b1.y; z[6] += b1.z; z[7] += b1.w;
+  }
+  if (e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU) {
+    if (e.aux) V8<TC>::store(reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col, z);
+    if (e.act == MMFD_ACT_GELU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z[q] = gelu_f(z[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z[q] = fmaxf(z[q], 0.0f);
+    }
+  } else if (e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD) {
+    float a[8];
+    V8<TC>::load(reinterpret_cast<const TC*>(e.aux) + row * e.ldaux + col, a);
+    if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z[q] *= gelu_grad_f(a[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z[q] = a[q] > 0.0f ? z[q] : 0.0f;
+    }
+  }
+  if (e.p > 0.0f) {
+    const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)col;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] = (mmfd_hash(seed, e.salt, base + q) < e.thr) ? 0.0f : z[q] * e.keep_scale;
+  }
+  if (e.residual) {
+    float r[8];
+    V8<TC>::load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] += r[q];
+  }
+  TC* cp = C + row * ldc + col;
+  if (e.beta != 0.0f) {
+    float c[8];
+    V8<TC>::load(cp, c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] += e.beta * c[q];
+  }
+  V8<TC>::store(cp, z);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -256,21 +330,32 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
           for (int r = 0; r < 4; ++r) ct[(i * 16 + 4 * g + r) * LDC + wn * 64 + j * 16 + ci] = acc[i][j][r];
     }
     __syncthreads();
-    for (int idx = tid; idx < 64 * (BN / 4); idx += NT) {
-      const int lr = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+    // 64 rows x 16 groups of 8 columns; 2 groups per thread
+    for (int idx = tid; idx < 64 * (BN / 8); idx += NT) {
+      const int lr = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
       const int64_t row = m0 + qtr * 64 + lr;
-      const int64_t col = n0 + c4;
+      const int64_t col = n0 + c8;
       if (row >= M || col >= N) continue;
-      const float4 v = *reinterpret_cast<const float4*>(ct + lr * LDC + c4);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
+      const float* src = ct + lr * LDC + c8;
+      const float4 a4 = *reinterpret_cast<const float4*>(src), b4 = *reinterpret_cast<const float4*>(src + 4);
+      float vv[8] = {alpha * a4.x, alpha * a4.y, alpha * a4.z, alpha * a4.w,
+                     alpha * b4.x, alpha * b4.y, alpha * b4.z, alpha * b4.w};
+      const bool full = col + 8 <= N;
       if (slab) {
+        if (full && (N % 4) == 0) {
+          *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          *reinterpret_cast<float4*>(slab + row * N + col + 4) = make_float4(vv[4], vv[5], vv[6], vv[7]);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (col + q < N) slab[row * N + col + q] = alpha * vv[q];
+          for (int q = 0; q < 8; ++q)
+            if (col + q < N) slab[row * N + col + q] = vv[q];
+        }
+      } else if (full && e.vec) {
+        epilogue_store8<TC>(e, C, ldc, N, row, col, vv, seed);
       } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (col + q < N) epilogue_store<TC>(e, C, ldc, N, row, col + q, alpha * vv[q], seed);
+        for (int q = 0; q < 8; ++q)
+          if (col + q < N) epilogue_store<TC>(e, C, ldc, N, row, col + q, vv[q], seed);
       }
     }
     __syncthreads();
@@ -282,6 +367,18 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, T
                                      int64_t ldc, int64_t M, int64_t N, EpiArgs e) {
   const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
   const int64_t total = M * N;
+  if (e.vec && (N % 8) == 0) {
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total / 8; g += (int64_t)gridDim.x * blockDim.x) {
+      float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < splits; ++s) {
+        const float* p = ws + (int64_t)s * total + g * 8;
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        z[0] += a.x; z[1] += a.y; z[2] += a.z; z[3] += a.w; z[4] += b.x; z[5] += b.y; z[6] += b.z; z[7] += b.w;
+      }
+      epilogue_store8<TC>(e, C, ldc, N, (g * 8) / N, (g * 8) % N, z, seed);
+    }
+    return;
+  }
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     float z = 0.f;
@@ -397,6 +494,14 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   e.ldaux = a.ep.ldaux; e.act = act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
   e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
   e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta;
+  {
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    bool v = al(a.C) && (a.ldc % 8) == 0;
+    if (a.ep.residual) v = v && al(a.ep.residual) && (a.ep.ldr % 8) == 0;
+    if (a.ep.aux) v = v && al(a.ep.aux) && (a.ep.ldaux % 8) == 0;
+    if (a.ep.bias) v = v && al(a.ep.bias);
+    e.vec = v ? 1 : 0;
+  }
 
   const bool bf = a.dtype == MMFD_BF16, cbf = a.c_dtype == MMFD_BF16;
   if (!mfma_ok(a)) {
