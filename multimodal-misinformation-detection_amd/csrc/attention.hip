@@ -18,6 +18,7 @@
 #include "common.h"
 #include <algorithm>
 #include <math.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -477,6 +478,299 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
   }
 }
 
+// =================================================================================================
+// v2 kernels (bf16, Lq and Lk <= 256): one workgroup of 8 waves per (b, h). The whole K/V (forward,
+// dQ) or Q/dO (dK/dV) of the head is staged in LDS ONCE and every wave sweeps 16-row blocks against
+// it: no per-block restaging, no repeated K/V reads from L2, and the forward softmax is single pass
+// (all 16 S^T subtiles stay in registers, so no online rescaling).
+// =================================================================================================
+constexpr int V2_LMAX = 256;
+constexpr int V2_THREADS = 512;
+
+template <typename T, int D, bool TR>
+__device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base, int64_t st, int64_t nrows,
+                                          int nrows_pad, int tid, int dreal) {
+  constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
+  for (int c = tid; c < nrows_pad * NCH; c += V2_THREADS) {
+    const int r = c / NCH, ch = c % NCH;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nrows && ch * EPC < dreal) v = *reinterpret_cast<const uint4*>(base + (int64_t)r * st + ch * EPC);
+    const int off = TR ? (r * AT<T, D>::RB + (tr_chunk<T, D>(r, ch) << 4)) : row_off<T, D>(r, ch);
+    *reinterpret_cast<uint4*>(lds + off) = v;
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
+  using T = bf16;
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  char* k_img = smem;
+  char* v_img = smem + lk_pad * C::RB;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  stage_all<T, D, false>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, tid, p.D);
+  stage_all<T, D, true>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
+  __syncthreads();
+  const int nks = lk_pad / 16;  // 16-key subtiles (even)
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
+  const int nqb = (int)((p.Lq + 15) / 16);
+  for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
+    const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
+    uint4 qf[C::KCH];
+    load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+    f32x4 s[V2_LMAX / 16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int ks = 0; ks < V2_LMAX / 16; ++ks) {
+      if (ks < nks) {
+        s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(k_img, ks, kc, lane), qf[kc]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t key = ks * 16 + 4 * g + r;
+          float v = s[ks][r] * p.scale;
+          if (key >= p.Lk) v = -INFINITY;
+          else if (p.key_bias || p.rel_bias) v += bias_at(p, b, h, myq < p.Lq ? myq : 0, key);
+          s[ks][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < V2_LMAX / 16; ++ks) {
+      if (ks < nks) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(s[ks][r] - mx);
+          sum += e;
+          float pe = e;
+          if (p.p > 0.f) {
+            const int64_t key = ks * 16 + 4 * g + r;
+            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+            pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
+          }
+          s[ks][r] = pe;
+        }
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    f32x4 o[C::DT];
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < V2_LMAX / 32; ++c) {
+      if (2 * c < nks) {
+        const uint4 a = pack_acc<T>(s, c);
+#pragma unroll
+        for (int d = 0; d < C::DT; ++d) Mma<T>::run(o[d], a, tr_frag<T, D>(v_img, c, d, lane));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float lr = __shfl(sum, 4 * g + r, 64);
+      const int64_t q = q0 + 4 * g + r;
+      const float inv = 1.0f / lr;
+      if (q < p.Lq) {
+#pragma unroll
+        for (int d = 0; d < C::DT; ++d)
+          if (d * 16 + li < p.D) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
+      }
+    }
+    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = mx + __logf(sum);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(V2_THREADS) attn_dkdv_v2_kernel(AttnP p) {
+  using T = bf16;
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lq_pad = (int)((p.Lq + 31) & ~31);
+  const int img = lq_pad * C::RB;
+  char* q_row = smem;
+  char* q_tr = smem + img;
+  char* do_row = smem + 2 * img;
+  char* do_tr = smem + 3 * img;
+  float* s_lse = reinterpret_cast<float*>(smem + 4 * img);
+  float* s_delta = s_lse + V2_LMAX;
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
+  stage_all<T, D, false>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, true>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, false>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, true>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  for (int i = tid; i < lq_pad; i += V2_THREADS) {
+    s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] : INFINITY;
+    s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
+  }
+  __syncthreads();
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
+  T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * p.D;
+  T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const int nkb = (int)((p.Lk + 15) / 16);
+  const int nqc = lq_pad / 32;  // 32-query chunks
+  for (int kbk = wave; kbk < nkb; kbk += V2_THREADS / 64) {
+    const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
+    uint4 kf[C::KCH], vf[C::KCH];
+    load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
+    load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    f32x4 dk[C::DT], dv[C::DT];
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+    for (int qc = 0; qc < nqc; ++qc) {
+      f32x4 pd[2], ds[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qs = 2 * qc + h2;
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+        for (int kc = 0; kc < C::KCH; ++kc) {
+          Mma<T>::run(sv, row_frag<T, D>(q_row, qs, kc, lane), kf[kc]);
+          Mma<T>::run(dp, row_frag<T, D>(do_row, qs, kc, lane), vf[kc]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lq = qs * 16 + 4 * g + r;
+          float pr = 0.f;
+          if (mykey < p.Lk) {
+            float sc = sv[r] * p.scale;
+            if ((p.key_bias || p.rel_bias) && lq < p.Lq) sc += bias_at(p, b, h, lq, mykey);
+            pr = __expf(sc - s_lse[lq]);
+          }
+          float z = 1.f;
+          if (p.p > 0.f) {
+            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + lq) * p.Lk + mykey));
+            z = (hsh < p.thr) ? 0.f : p.keep_scale;
+          }
+          pd[h2][r] = pr * z;
+          ds[h2][r] = pr * (dp[r] * z - s_delta[lq]);
+        }
+      }
+      const uint4 ap = pack_acc<T>(pd, 0);
+      const uint4 as = pack_acc<T>(ds, 0);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        Mma<T>::run(dv[d], ap, tr_frag<T, D>(do_tr, qc, d, lane));
+        Mma<T>::run(dk[d], as, tr_frag<T, D>(q_tr, qc, d, lane));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t key = k0 + 4 * g + r;
+      if (key < p.Lk) {
+#pragma unroll
+        for (int d = 0; d < C::DT; ++d) {
+          if (d * 16 + li >= p.D) continue;
+          T* pk = dkb + key * p.dk_st + d * 16 + li;
+          T* pv = dvb + key * p.dv_st + d * 16 + li;
+          float vk = dk[d][r] * p.scale, vv = dv[d][r];
+          if (p.acc_dkv) { vk += to_f32(*pk); vv += to_f32(*pv); }
+          *pk = from_f32<T>(vk);
+          *pv = from_f32<T>(vv);
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
+  using T = bf16;
+  using C = AT<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  const int img = lk_pad * C::RB;
+  char* k_row = smem;
+  char* k_tr = smem + img;
+  char* v_row = smem + 2 * img;
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  stage_all<T, D, false>(k_row, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
+  stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
+  stage_all<T, D, false>(v_row, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
+  __syncthreads();
+  const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
+  const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
+  T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
+  const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const int nqb = (int)((p.Lq + 15) / 16);
+  const int nkc = lk_pad / 32;
+  for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
+    const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
+    uint4 qf[C::KCH], dof[C::KCH];
+    load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+    load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
+    const float lse = myq < p.Lq ? p.lse[bh * p.Lq + myq] : INFINITY;
+    const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+    f32x4 dq[C::DT];
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc2 = 0; kc2 < nkc; ++kc2) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int ks = 2 * kc2 + h2;
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+        for (int kc = 0; kc < C::KCH; ++kc) {
+          Mma<T>::run(sv, row_frag<T, D>(k_row, ks, kc, lane), qf[kc]);
+          Mma<T>::run(dp, row_frag<T, D>(v_row, ks, kc, lane), dof[kc]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t key = ks * 16 + 4 * g + r;
+          float pr = 0.f;
+          if (key < p.Lk) {
+            float sc = sv[r] * p.scale;
+            if ((p.key_bias || p.rel_bias) && myq < p.Lq) sc += bias_at(p, b, h, myq, key);
+            pr = __expf(sc - lse);
+          }
+          float z = 1.f;
+          if (p.p > 0.f) {
+            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+            z = (hsh < p.thr) ? 0.f : p.keep_scale;
+          }
+          ds[h2][r] = pr * (dp[r] * z - dlt);
+        }
+      }
+      const uint4 as = pack_acc<T>(ds, 0);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) Mma<T>::run(dq[d], as, tr_frag<T, D>(k_tr, kc2, d, lane));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t q = q0 + 4 * g + r;
+      if (q < p.Lq) {
+#pragma unroll
+        for (int d = 0; d < C::DT; ++d) {
+          if (d * 16 + li >= p.D) continue;
+          T* pq = dqb + q * p.dq_st + d * 16 + li;
+          float vq = dq[d][r] * p.scale;
+          if (p.acc_dq) vq += to_f32(*pq);
+          *pq = from_f32<T>(vq);
+        }
+      }
+    }
+  }
+}
+
 int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "attn: bad dtype");
   MMFD_CHECK_ARG(a.D > 0 && a.D <= 64, "attn: head_dim %lld unsupported (<= 64)", (long long)a.D);
@@ -513,6 +807,37 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   return 0;
 }
 
+template <int D>
+void set_lds_attr(const void* fn, int bytes) {
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+template <int D>
+void launch_fwd_v2(const AttnP& p, hipStream_t s) {
+  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  const int lds = 2 * lk_pad * AT<bf16, D>::RB;
+  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>), 2 * V2_LMAX * AT<bf16, D>::RB), true);
+  (void)once;
+  hipLaunchKernelGGL((attn_fwd_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds, s, p);
+}
+
+template <int D>
+void launch_bwd_v2(const AttnP& p, hipStream_t s) {
+  const int64_t rows = p.B * p.H * p.Lq;
+  constexpr int nch = AT<bf16, D>::NCH;
+  hipLaunchKernelGGL((attn_delta_kernel<bf16, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
+  const int lq_pad = (int)((p.Lq + 31) & ~31), lk_pad = (int)((p.Lk + 31) & ~31);
+  const int lds1 = 4 * lq_pad * AT<bf16, D>::RB + 2 * V2_LMAX * 4;
+  const int lds2 = 3 * lk_pad * AT<bf16, D>::RB;
+  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<D>),
+                                      4 * V2_LMAX * AT<bf16, D>::RB + 2 * V2_LMAX * 4),
+                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>), 3 * V2_LMAX * AT<bf16, D>::RB),
+                      true);
+  (void)once;
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds1, s, p);
+  hipLaunchKernelGGL((attn_dq_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
+}
+
 template <typename T, int D>
 void launch_fwd(const AttnP& p, hipStream_t s) {
   dim3 grid((unsigned)((p.Lq + 63) / 64), (unsigned)(p.B * p.H));
@@ -542,7 +867,9 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
+  const bool v2 = a->dtype == MMFD_BF16 && p.Lk <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  if (v2) { if (a->D > 32) launch_fwd_v2<64>(p, s); else launch_fwd_v2<32>(p, s); }
+  else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_fwd");
   return 0;
@@ -555,7 +882,9 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
+  const bool v2 = a->dtype == MMFD_BF16 && p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  if (v2) { if (a->D > 32) launch_bwd_v2<64>(p, s); else launch_bwd_v2<32>(p, s); }
+  else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_bwd");
   return 0;

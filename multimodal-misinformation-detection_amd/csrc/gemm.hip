@@ -595,20 +595,31 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ldx, int6
 }  // namespace
 
 // pass 2, shared with the LayerNorm backward: out[c] = beta*out[c] + sum_p part[p*stride + c];
-// block = 64 columns x 4 waves splitting the partials, combined through LDS.
-__global__ void __launch_bounds__(256) mmfd_reduce_partials_kernel(const float* __restrict__ part, int nparts,
-                                                                   int64_t stride, int64_t N, float* __restrict__ out,
-                                                                   float beta) {
-  __shared__ float red[4][64];
+// block = 64 columns x 16 waves splitting the partials (4 independent loads in flight per lane),
+// combined through LDS in a fixed order (deterministic).
+__global__ void __launch_bounds__(1024) mmfd_reduce_partials_kernel(const float* __restrict__ part, int nparts,
+                                                                    int64_t stride, int64_t N, float* __restrict__ out,
+                                                                    float beta) {
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (col < N)
-    for (int p = wave; p < nparts; p += 4) s += part[(int64_t)p * stride + col];
-  red[wave][lane] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    int p = wave;
+    for (; p + 48 < nparts; p += 64) {
+      s0 += part[(int64_t)p * stride + col];
+      s1 += part[(int64_t)(p + 16) * stride + col];
+      s2 += part[(int64_t)(p + 32) * stride + col];
+      s3 += part[(int64_t)(p + 48) * stride + col];
+    }
+    for (; p < nparts; p += 16) s0 += part[(int64_t)p * stride + col];
+  }
+  red[wave][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wave == 0 && col < N) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
     out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
   }
 }
@@ -637,7 +648,7 @@ extern "C" int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64
     else
       hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)X, ldx, M, N, rpb, (float*)workspace);
   }
-  hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s,
+  hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s,
                      (const float*)workspace, nparts, N, N, out, beta);
   MMFD_CHECK_LAUNCH("colsum");
   return 0;

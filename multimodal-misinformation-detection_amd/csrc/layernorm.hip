@@ -207,10 +207,10 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
                        (float*)dx_drop, p, thr, seed, salt, (float*)workspace);
   // part layout [block][2][width]: gamma partials at offset 0, beta partials at +width, stride 2*width
   if (dgamma)
-    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(256), 0, s,
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(1024), 0, s,
                        (const float*)workspace, nblocks, 2 * width, width, dgamma, beta_acc);
   if (dbeta)
-    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(256), 0, s,
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((width + 63) / 64)), dim3(1024), 0, s,
                        (const float*)workspace + width, nblocks, 2 * width, width, dbeta, beta_acc);
   MMFD_CHECK_LAUNCH("layernorm_bwd");
   return 0;

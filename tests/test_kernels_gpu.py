@@ -154,7 +154,8 @@ def _attn_ref(q, k, v, H, scale, key_bias=None, keep=None, p=0.0):
 
 
 ATTN_CASES = [(2, 4, 128, 128, 64), (2, 8, 197, 197, 32), (3, 2, 13, 29, 64), (2, 8, 128, 197, 32),
-              (1, 12, 70, 70, 64), (2, 4, 21, 33, 8), (2, 2, 40, 40, 16), (1, 3, 65, 130, 48)]
+              (1, 12, 70, 70, 64), (2, 4, 21, 33, 8), (2, 2, 40, 40, 16), (1, 3, 65, 130, 48),
+              (1, 2, 260, 300, 64), (2, 16, 256, 256, 64)]  # L > 256 exercises the streaming kernels
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
