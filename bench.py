@@ -47,6 +47,21 @@ def cpu_baseline(steps=2, batch=4):
                       f"1 warmup + {steps} timed steps, {dt:.2f} s/step"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (tools/profile.sh ->
+    profiles/<tag>_hbm_traffic.json: FETCH_SIZE x2 + WRITE_SIZE), or None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    if k is None:
+        return None, os.path.basename(files[-1])
+    return int(k["traffic_bytes_per_dispatch"]), os.path.basename(files[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,13 +118,14 @@ def main():
     loss_val = loss[0].item()
 
     prof = probe.summary()
-    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    dom = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     dom_name, d = dom
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
     gemm_ms = sum(v["ms"] for v in prof.values()) / args.steps
     gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
 
+    traffic, traffic_src = pmc_traffic(dom_name)
     if rank == 0:
         step_tflops = pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3
         out = {
@@ -121,7 +137,8 @@ def main():
                        "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
                          "launches_per_step": d["launches"] // args.steps,
                          "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
                          "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])},

@@ -485,13 +485,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 // (all 16 S^T subtiles stay in registers, so no online rescaling).
 // =================================================================================================
 constexpr int V2_LMAX = 256;
-constexpr int V2_THREADS = 512;
+constexpr int V2_THREADS = 256;       // forward / dQ: 4 waves, several workgroups per CU
+constexpr int V2_DKDV_THREADS = 512;  // dK/dV: its Q/dO images allow one workgroup per CU at L ~ 200
 
-template <typename T, int D, bool TR>
+template <typename T, int D, bool TR, int NTH = V2_THREADS>
 __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base, int64_t st, int64_t nrows,
                                           int nrows_pad, int tid, int dreal) {
   constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
-  for (int c = tid; c < nrows_pad * NCH; c += V2_THREADS) {
+  for (int c = tid; c < nrows_pad * NCH; c += NTH) {
     const int r = c / NCH, ch = c % NCH;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r < nrows && ch * EPC < dreal) v = *reinterpret_cast<const uint4*>(base + (int64_t)r * st + ch * EPC);
@@ -502,20 +503,21 @@ __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base,
 
 template <int D>
 __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
+  // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax over
+  // 64-key chunks (few live registers -> several workgroups per CU overlap staging and compute)
   using T = bf16;
   using C = AT<T, D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  const int lk_pad = (int)((p.Lk + 63) & ~63);
   char* k_img = smem;
   char* v_img = smem + lk_pad * C::RB;
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   stage_all<T, D, false>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, tid, p.D);
   stage_all<T, D, true>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
   __syncthreads();
-  const int nks = lk_pad / 16;  // 16-key subtiles (even)
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
@@ -523,61 +525,71 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH];
     load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
-    f32x4 s[V2_LMAX / 16];
-    float mx = -INFINITY;
+    const uint64_t hbase = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[C::DT];
 #pragma unroll
-    for (int ks = 0; ks < V2_LMAX / 16; ++ks) {
-      if (ks < nks) {
+    for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < lk_pad; k0 += 64) {
+      const char* kc_img = k_img + k0 * C::RB;
+      const char* vc_img = v_img + k0 * C::RB;
+      f32x4 s[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
         s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(k_img, ks, kc, lane), qf[kc]);
+        for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t key = ks * 16 + 4 * g + r;
+          const int key = k0 + ks * 16 + 4 * g + r;
           float v = s[ks][r] * p.scale;
           if (key >= p.Lk) v = -INFINITY;
           else if (p.key_bias || p.rel_bias) v += bias_at(p, b, h, myq < p.Lq ? myq : 0, key);
           s[ks][r] = v;
           mx = fmaxf(mx, v);
         }
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = __expf(m - mnew);
+      float rs = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < V2_LMAX / 16; ++ks) {
-      if (ks < nks) {
+      for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(s[ks][r] - mx);
-          sum += e;
+          const float e = __expf(s[ks][r] - mnew);
+          rs += e;
           float pe = e;
           if (p.p > 0.f) {
-            const int64_t key = ks * 16 + 4 * g + r;
-            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+            const uint32_t hsh = mmfd_hash(seed, p.salt, hbase + (uint64_t)(k0 + ks * 16 + 4 * g + r));
             pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
           }
           s[ks][r] = pe;
         }
+      lsum = lsum * alpha + rs;  // per-lane partial over this lane's keys; reduced at the end
+      m = mnew;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+        for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
       }
-    }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    f32x4 o[C::DT];
 #pragma unroll
-    for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < V2_LMAX / 32; ++c) {
-      if (2 * c < nks) {
+      for (int c = 0; c < 2; ++c) {
         const uint4 a = pack_acc<T>(s, c);
 #pragma unroll
-        for (int d = 0; d < C::DT; ++d) Mma<T>::run(o[d], a, tr_frag<T, D>(v_img, c, d, lane));
+        for (int d = 0; d < C::DT; ++d) Mma<T>::run(o[d], a, tr_frag<T, D>(vc_img, c, d, lane));
       }
     }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float lr = __shfl(sum, 4 * g + r, 64);
+      const float lr = __shfl(lsum, 4 * g + r, 64);
       const int64_t q = q0 + 4 * g + r;
       const float inv = 1.0f / lr;
       if (q < p.Lq) {
@@ -586,12 +598,12 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
           if (d * 16 + li < p.D) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
       }
     }
-    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = mx + __logf(sum);
+    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = m + __logf(lsum);
   }
 }
 
 template <int D>
-__global__ void __launch_bounds__(V2_THREADS) attn_dkdv_v2_kernel(AttnP p) {
+__global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) {
   using T = bf16;
   using C = AT<T, D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -608,11 +620,11 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dkdv_v2_kernel(AttnP p) {
   float* s_delta = s_lse + V2_LMAX;
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
-  stage_all<T, D, false>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, true>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, false>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, true>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  for (int i = tid; i < lq_pad; i += V2_THREADS) {
+  stage_all<T, D, false, V2_DKDV_THREADS>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, true, V2_DKDV_THREADS>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, false, V2_DKDV_THREADS>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, true, V2_DKDV_THREADS>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  for (int i = tid; i < lq_pad; i += V2_DKDV_THREADS) {
     s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
   }
@@ -624,7 +636,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dkdv_v2_kernel(AttnP p) {
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const int nkb = (int)((p.Lk + 15) / 16);
   const int nqc = lq_pad / 32;  // 32-query chunks
-  for (int kbk = wave; kbk < nkb; kbk += V2_THREADS / 64) {
+  for (int kbk = wave; kbk < nkb; kbk += V2_DKDV_THREADS / 64) {
     const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
     uint4 kf[C::KCH], vf[C::KCH];
     load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
@@ -814,7 +826,7 @@ void set_lds_attr(const void* fn, int bytes) {
 
 template <int D>
 void launch_fwd_v2(const AttnP& p, hipStream_t s) {
-  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  const int lk_pad = (int)((p.Lk + 63) & ~63);
   const int lds = 2 * lk_pad * AT<bf16, D>::RB;
   static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>), 2 * V2_LMAX * AT<bf16, D>::RB), true);
   (void)once;
@@ -834,7 +846,7 @@ void launch_bwd_v2(const AttnP& p, hipStream_t s) {
                       set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>), 3 * V2_LMAX * AT<bf16, D>::RB),
                       true);
   (void)once;
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds1, s, p);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_DKDV_THREADS), lds1, s, p);
   hipLaunchKernelGGL((attn_dq_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
 }
 

@@ -13,11 +13,24 @@ import torch.distributed as dist
 from . import kernels as K
 
 
+def _pack(g, dst):
+    K.cast(g, torch.float32, out=dst)
+
+
+def _unpack(src, g, scale):
+    K.axpby(scale, src, 0.0, None, out=g)
+
+
 class GradAllReduce:
-    def __init__(self, bucket_mb: float = 64.0, group=None):
-        self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
+    """`pack(grad, flat_slice)` / `unpack(flat_slice, grad, scale)` default to the HIP cast/axpby
+    kernels; they are parameters only so the bucketing + collective logic can be exercised on the
+    CPU (gloo) in tests."""
+
+    def __init__(self, bucket_mb: float = 64.0, group=None, pack=_pack, unpack=_unpack):
+        self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
         self.group = group
         self._bufs = {}
+        self._pack, self._unpack = pack, unpack
 
     def _buckets(self, grads):
         bucket, n = [], 0
@@ -42,12 +55,12 @@ class GradAllReduce:
                 buf = self._bufs[i] = torch.empty(n, device=bucket[0].device, dtype=torch.float32)
             off = 0
             for g in bucket:
-                K.cast(g, torch.float32, out=buf[off:off + g.numel()])
+                self._pack(g, buf[off:off + g.numel()])
                 off += g.numel()
             works.append((dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True), bucket, buf))
         for w, bucket, buf in works:
             w.wait()
             off = 0
             for g in bucket:
-                K.axpby(1.0 / world, buf[off:off + g.numel()], 0.0, None, out=g)
+                self._unpack(buf[off:off + g.numel()], g, 1.0 / world)
                 off += g.numel()

@@ -1,0 +1,66 @@
+"""Data-parallel gradient averaging (mmfd.dp.GradAllReduce) over gloo, world_size 2, on the CPU.
+
+The HIP pack/unpack kernels are swapped for torch copies here (no GPU in this container); the
+bucketing, the asynchronous all-reduce and the 1/world scaling are the code under test.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pack(g, dst):
+    dst.copy_(g.reshape(-1).float())
+
+
+def _unpack(src, g, scale):
+    g.copy_((src * scale).view(g.shape))
+
+
+def _worker(rank, world, port, bucket_mb, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.dp import GradAllReduce
+
+        shapes = [(7, 5), (300,), (64, 33), (1,), (129, 3)]
+        params = []
+        for i, s in enumerate(shapes):
+            p = torch.zeros(s, requires_grad=True)
+            g = torch.Generator().manual_seed(1000 * rank + i)
+            p.grad = torch.randn(s, generator=g)
+            params.append(p)
+        params.append(torch.zeros(3, requires_grad=True))  # no grad: skipped
+        GradAllReduce(bucket_mb=bucket_mb, pack=_pack, unpack=_unpack).allreduce_grads(params)
+        q.put((rank, [p.grad.clone() if p.grad is not None else None for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb", [64.0, 0.001])  # one bucket / many small buckets
+def test_grad_allreduce_gloo_world2(bucket_mb):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shapes = [(7, 5), (300,), (64, 33), (1,), (129, 3)]
+    for i, s in enumerate(shapes):
+        want = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * r + i)) for r in range(world)) / world
+        for r in range(world):
+            torch.testing.assert_close(res[r][i], want, rtol=1e-6, atol=1e-6)
+    assert res[0][-1] is None and res[1][-1] is None

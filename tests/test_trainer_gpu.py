@@ -1,0 +1,44 @@
+"""Whole training step (BERT + ViT + fusion head + AdamW, FusionTrainer) on the HIP path vs the
+CPU oracle's step (oracle/train_step.py, restating train.py:123-188 with trainable encoders).
+
+Tolerances: fp32 — losses 1e-3 abs (north_star), every parameter gradient 2e-3 relative to that
+tensor's max |grad|, over two consecutive steps (the second starts from AdamW-updated weights);
+bf16 — losses 5e-2 abs, gradients 0.1 relative (bf16 operands, fp32 accumulation/master weights).
+"""
+import pytest
+import torch
+
+from tests.smoke_impl import TINY, build_pair, compare_step, tiny_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_train_step_fp32_matches_oracle(dropout):
+    tr, ref = build_pair("fp32", dropout=dropout)
+    for s in (1, 2):
+        compare_step(tr, ref, tiny_batch(3, seed=s), loss_tol=1e-3, grad_rtol=2e-3)
+
+
+def test_train_step_fp32_wider_matches_oracle():
+    cfg = dict(TINY, D=128, heads=2, inter=256, seq=40, img=48, patch=16, embed=64, head_heads=8)
+    tr, ref = build_pair("fp32", dropout=0.1, cfg=cfg)
+    compare_step(tr, ref, tiny_batch(2, cfg=cfg, seed=3), loss_tol=1e-3, grad_rtol=2e-3)
+
+
+def test_train_step_bf16_close_to_oracle():
+    tr, ref = build_pair("bf16", dropout=0.0)
+    compare_step(tr, ref, tiny_batch(3, seed=4), loss_tol=5e-2, grad_rtol=0.1)
+
+
+def test_frozen_encoders_only_head_updates():
+    tr, _ = build_pair("fp32", dropout=0.0)
+    from mmfd.train import FusionTrainer
+
+    ft = FusionTrainer(tr.text_encoder, tr.image_encoder, tr.head, freeze_encoders=True, precision="fp32")
+    before = [p.detach().clone() for p in tr.text_encoder.parameters()]
+    hb = [p.detach().clone() for p in tr.head.parameters()]
+    ft.step({k: v.cuda() for k, v in tiny_batch(2, seed=9).items()})
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(before, tr.text_encoder.parameters()))
+    assert any(not torch.equal(a, b) for a, b in zip(hb, tr.head.parameters()))
