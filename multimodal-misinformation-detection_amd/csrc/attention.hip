@@ -66,7 +66,9 @@ __device__ __forceinline__ int row_off(int r, int c) {
 template <typename T, int D>
 __device__ __forceinline__ int tr_chunk(int r, int c) {
   if (sizeof(T) == 2) {
-    if (D == 64) return c ^ (2 * ((r >> 1) & 3));
+    // D = 64 (128-B rows): the ROW swizzle c ^ (r & 7) is also conflict-free for the transposed
+    // 8-row reads, so one image serves both kinds of read (DUAL below)
+    if (D == 64) return c ^ (r & 7);
     return c ^ (2 * ((r >> 2) & 1));
   }
   return c ^ (4 * ((r >> 2) & 1));
@@ -486,7 +488,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 // =================================================================================================
 constexpr int V2_LMAX = 256;
 constexpr int V2_THREADS = 256;       // forward / dQ: 4 waves, several workgroups per CU
-constexpr int V2_DKDV_THREADS = 512;  // dK/dV: its Q/dO images allow one workgroup per CU at L ~ 200
+constexpr int V2_DKDV_THREADS = 256;
+template <int D> struct V2 { static constexpr bool DUAL = (D == 64); };  // row image == transposed image
 
 template <typename T, int D, bool TR, int NTH = V2_THREADS>
 __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base, int64_t st, int64_t nrows,
@@ -612,18 +615,19 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const int lq_pad = (int)((p.Lq + 31) & ~31);
   const int img = lq_pad * C::RB;
+  constexpr bool DUAL = V2<D>::DUAL;
   char* q_row = smem;
-  char* q_tr = smem + img;
-  char* do_row = smem + 2 * img;
-  char* do_tr = smem + 3 * img;
-  float* s_lse = reinterpret_cast<float*>(smem + 4 * img);
+  char* do_row = smem + img;
+  char* q_tr = DUAL ? q_row : smem + 2 * img;
+  char* do_tr = DUAL ? do_row : smem + 3 * img;
+  float* s_lse = reinterpret_cast<float*>(smem + (DUAL ? 2 : 4) * img);
   float* s_delta = s_lse + V2_LMAX;
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   stage_all<T, D, false, V2_DKDV_THREADS>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, true, V2_DKDV_THREADS>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true, V2_DKDV_THREADS>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
   stage_all<T, D, false, V2_DKDV_THREADS>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, true, V2_DKDV_THREADS>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true, V2_DKDV_THREADS>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
   for (int i = tid; i < lq_pad; i += V2_DKDV_THREADS) {
     s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
@@ -710,12 +714,13 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const int lk_pad = (int)((p.Lk + 31) & ~31);
   const int img = lk_pad * C::RB;
+  constexpr bool DUAL = V2<D>::DUAL;
   char* k_row = smem;
-  char* k_tr = smem + img;
-  char* v_row = smem + 2 * img;
+  char* v_row = smem + img;
+  char* k_tr = DUAL ? k_row : smem + 2 * img;
   const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
   stage_all<T, D, false>(k_row, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
-  stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
   stage_all<T, D, false>(v_row, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
   __syncthreads();
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
@@ -839,11 +844,12 @@ void launch_bwd_v2(const AttnP& p, hipStream_t s) {
   constexpr int nch = AT<bf16, D>::NCH;
   hipLaunchKernelGGL((attn_delta_kernel<bf16, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
   const int lq_pad = (int)((p.Lq + 31) & ~31), lk_pad = (int)((p.Lk + 31) & ~31);
-  const int lds1 = 4 * lq_pad * AT<bf16, D>::RB + 2 * V2_LMAX * 4;
-  const int lds2 = 3 * lk_pad * AT<bf16, D>::RB;
+  constexpr int NI1 = V2<D>::DUAL ? 2 : 4, NI2 = V2<D>::DUAL ? 2 : 3;  // LDS images per kernel
+  const int lds1 = NI1 * lq_pad * AT<bf16, D>::RB + 2 * V2_LMAX * 4;
+  const int lds2 = NI2 * lk_pad * AT<bf16, D>::RB;
   static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<D>),
-                                      4 * V2_LMAX * AT<bf16, D>::RB + 2 * V2_LMAX * 4),
-                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>), 3 * V2_LMAX * AT<bf16, D>::RB),
+                                      NI1 * V2_LMAX * AT<bf16, D>::RB + 2 * V2_LMAX * 4),
+                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>), NI2 * V2_LMAX * AT<bf16, D>::RB),
                       true);
   (void)once;
   hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_DKDV_THREADS), lds1, s, p);

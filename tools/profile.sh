@@ -13,6 +13,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
   python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline > $OUT/bench_trace.json
+if [ "${PMC:-1}" = 0 ]; then exit 0; fi
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- \
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.json
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- \
