@@ -13,6 +13,7 @@
 // The three nn.Linear products are (TA,TB) = (0,0) forward, (0,1) grad-input, (1,1) grad-weight.
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace {
 
@@ -362,6 +363,208 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
   }
 }
 
+// =================================================================================================
+// bf16 256x256 kernel ("G8"): 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns four 64x32 quadrants
+// (mq, nq): rows mq*128 + wr*64 + [0,64), cols nq*128 + wc*32 + [0,32). Each K-tile (64 bf16) is
+// staged as four 16-KB half-tiles (A rows [0,128) / [128,256), B cols [0,128) / [128,256)) into
+// one of two LDS buffers by LDS-DMA, and consumed in four phases, one quadrant (16 MFMAs) each:
+//   phase 0: (0,0) reads A-h0, B-h0   phase 1: (0,1) reads B-h1
+//   phase 2: (1,1) reads A-h1         phase 3: (1,0) reads B-h0
+// Every phase refills the half-tile whose last read was the previous phase (one half-tile = two
+// DMA pieces per wave), so three half-tiles stay in flight across the barriers; the only wait is
+// a counted vmcnt(6) in phase 3. The two wave rows run one barrier apart (ping-pong): while one
+// row issues its LDS reads and DMA the other row's MFMAs run.
+// =================================================================================================
+constexpr int G8_HALF = 16384, G8_LDS = 8 * G8_HALF;  // 2 buffers x 4 half-tiles = 128 KB
+constexpr int G8_BM = 256, G8_BN = 256, G8_BK = 64;
+
+__device__ __forceinline__ void g8_pre_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS reads retired (WAR vs the next refill)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void g8_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void g8_frag_a(uint4 (&a)[4][2], const char* img, int wr, int lane) {
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<bf16, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
+}
+template <int LAYOUT>
+__device__ __forceinline__ void g8_frag_b(uint4 (&b)[2][2], const char* img, int wc, int lane) {
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j][kc] = load_frag<bf16, LAYOUT, 128>(img, wc * 2 + j, kc, lane);
+}
+__device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2], const uint4 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) Mma<bf16>::run(acc[i][j], a[i][kc], b[j][kc]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int TA, int TB, typename TC>
+__global__ void __launch_bounds__(NT, 1)
+gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+               TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
+               float alpha, int tiles_per_split, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int tile = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  const int64_t m0 = (int64_t)(tile / gx) * G8_BM, n0 = (int64_t)(tile % gx) * G8_BN;
+  const int nkt_total = (int)((K + G8_BK - 1) / G8_BK);
+  const int kt0 = blockIdx.z * tiles_per_split;
+  const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * 2);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * 2);
+  Fill<bf16, TA, 128, 2> fa0, fa1;
+  Fill<bf16, TB, 128, 2> fb0, fb1;
+  fa0.init(lda, m0, M, wave, lane);
+  fa1.init(lda, m0 + 128, M, wave, lane);
+  fb0.init(ldb, n0, N, wave, lane);
+  fb1.init(ldb, n0 + 128, N, wave, lane);
+
+  // half-tile h of K-tile t: 0 = A-h0, 1 = A-h1, 2 = B-h0, 3 = B-h1; buffer t & 1
+  auto img = [&](int t, int h) -> char* { return smem + ((t & 1) * 4 + h) * G8_HALF; };
+  auto issue = [&](int h, int t) {
+    const int64_t k0 = (int64_t)(kt0 + t) * G8_BK;
+    const bool tail = k0 + G8_BK > K;
+    if (h < 2) {
+      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * 2);
+      if (h == 0) fa0.issue(rsa, img(t, 0), so, tail, k0, K, wave, lane);
+      else fa1.issue(rsa, img(t, 1), so, tail, k0, K, wave, lane);
+    } else {
+      const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * 2);
+      if (h == 2) fb0.issue(rsb, img(t, 2), so, tail, k0, K, wave, lane);
+      else fb1.issue(rsb, img(t, 3), so, tail, k0, K, wave, lane);
+    }
+  };
+
+  if (nk > 0) {
+    issue(0, 0); issue(3, 0); issue(1, 0); issue(2, 0);
+    if (nk > 1) {
+      issue(0, 1); issue(3, 1); issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  g8_barrier();
+  if (wr == 1) g8_barrier();  // stagger the second wave row by one barrier
+
+  uint4 fa[4][2], fb[2][2];
+  for (int t = 0; t < nk; ++t) {
+    // phase 0: quadrant (0,0)
+    g8_frag_a<TA>(fa, img(t, 0), wr, lane);
+    g8_frag_b<TB>(fb, img(t, 2), wc, lane);
+    if (t + 1 < nk) issue(2, t + 1);
+    g8_pre_barrier();
+    g8_mma(acc[0][0], fa, fb);
+    g8_barrier();
+    // phase 1: quadrant (0,1)
+    g8_frag_b<TB>(fb, img(t, 3), wc, lane);
+    if (t + 2 < nk) issue(0, t + 2);
+    g8_pre_barrier();
+    g8_mma(acc[0][1], fa, fb);
+    g8_barrier();
+    // phase 2: quadrant (1,1)
+    g8_frag_a<TA>(fa, img(t, 1), wr, lane);
+    if (t + 2 < nk) issue(3, t + 2);
+    g8_pre_barrier();
+    g8_mma(acc[1][1], fa, fb);
+    g8_barrier();
+    // phase 3: quadrant (1,0); K-tile t+1 must have landed before the next phase reads it
+    g8_frag_b<TB>(fb, img(t, 2), wc, lane);
+    if (t + 2 < nk) {
+      issue(1, t + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    g8_pre_barrier();
+    g8_mma(acc[1][0], fa, fb);
+    g8_barrier();
+  }
+  if (wr == 0) g8_barrier();  // re-align the wave rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: four passes of 64 rows (quadrant row mq = q >> 1 of wave row wr = q & 1)
+  constexpr int LDC = G8_BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
+  const int g = lane >> 4, ci = lane & 15;
+  const uint64_t seed = (!ws && e.p > 0.0f) ? *e.seed : 0ull;
+  float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (wr == (q & 1)) {
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ct[(i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[q >> 1][nq][i][j][r];
+    }
+    __syncthreads();
+    const int64_t rbase = m0 + (q >> 1) * 128 + (q & 1) * 64;
+    for (int idx = tid; idx < 64 * (G8_BN / 8); idx += NT) {
+      const int lr = idx / (G8_BN / 8), c8 = (idx % (G8_BN / 8)) * 8;
+      const int64_t row = rbase + lr, col = n0 + c8;
+      if (row >= M || col >= N) continue;
+      const float* src = ct + lr * LDC + c8;
+      const float4 a4 = *reinterpret_cast<const float4*>(src), b4 = *reinterpret_cast<const float4*>(src + 4);
+      float vv[8] = {alpha * a4.x, alpha * a4.y, alpha * a4.z, alpha * a4.w,
+                     alpha * b4.x, alpha * b4.y, alpha * b4.z, alpha * b4.w};
+      const bool full = col + 8 <= N;
+      if (slab) {
+        if (full && (N % 4) == 0) {
+          *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          *reinterpret_cast<float4*>(slab + row * N + col + 4) = make_float4(vv[4], vv[5], vv[6], vv[7]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (col + u < N) slab[row * N + col + u] = vv[u];
+        }
+      } else if (full && e.vec) {
+        epilogue_store8<TC>(e, C, ldc, N, row, col, vv, seed);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (col + u < N) epilogue_store<TC>(e, C, ldc, N, row, col + u, vv[u], seed);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
                                      int64_t ldc, int64_t M, int64_t N, EpiArgs e) {
@@ -421,6 +624,31 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
                      a.alpha, tps, e);
 }
 
+template <int TA, int TB, typename TC>
+void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s) {
+  dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<TA, TB, TC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm256_kernel<TA, TB, TC>), grid, dim3(NT), G8_LDS, s, (const bf16*)a.A, a.lda,
+                     (const bf16*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e);
+}
+
+template <typename TC>
+void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s) {
+  if (!a.trans_a && !a.trans_b) launch_g8<0, 0, TC>(a, e, ws, splits, tps, s);
+  else if (!a.trans_a && a.trans_b) launch_g8<0, 1, TC>(a, e, ws, splits, tps, s);
+  else if (a.trans_a && !a.trans_b) launch_g8<1, 0, TC>(a, e, ws, splits, tps, s);
+  else launch_g8<1, 1, TC>(a, e, ws, splits, tps, s);
+}
+
+bool use_g8(const mmfd_gemm_args& a) {
+  static const bool off = getenv("MMFD_GEMM_V1") != nullptr;
+  return a.dtype == MMFD_BF16 && !off;
+}
+
 template <typename T, typename TC>
 void dispatch_layout(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps,
                      hipStream_t s) {
@@ -447,11 +675,23 @@ bool mfma_ok(const mmfd_gemm_args& a) {
 
 int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
   const int T = (a.dtype == MMFD_BF16) ? 64 : 32;
-  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int64_t nkt = (a.K + T - 1) / T;
   int splits = 1;
-  if (a.splits > 0) splits = a.splits;
-  else if (tiles < 200 && nkt >= 16) {
+  if (use_g8(a)) {
+    // one 256x256 block per CU: pick the split count that minimises rounds-of-256 per unit of work
+    const int64_t tiles = ((a.M + G8_BM - 1) / G8_BM) * ((a.N + G8_BN - 1) / G8_BN);
+    if (a.splits > 0) splits = a.splits;
+    else if (nkt >= 16 && tiles < 256) {
+      double best = 1e30;
+      const int smax = (int)std::min<int64_t>(32, nkt / 8);
+      for (int sp = 1; sp <= smax; ++sp) {
+        const double cost = (double)((tiles * sp + 255) / 256) / sp + (sp > 1 ? 0.05 : 0.0) + 0.004 * sp;
+        if (cost < best) { best = cost; splits = sp; }
+      }
+    }
+  } else if (a.splits > 0) splits = a.splits;
+  else if (((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) < 200 && nkt >= 16) {
+    const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     splits = (int)((384 + tiles - 1) / tiles);
     splits = (int)std::min<int64_t>(splits, nkt / 8);
     splits = std::min(splits, 16);
@@ -523,7 +763,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need)) {
     // shrink to what the workspace allows
     const int64_t per = a.M * a.N * 4;
-    int fit = (a.workspace && per > 0) ? (int)std::min<int64_t>(a.workspace_bytes / per, 16) : 1;
+    int fit = (a.workspace && per > 0) ? (int)std::min<int64_t>(a.workspace_bytes / per, 32) : 1;
     splits = fit > 1 ? std::min(splits, fit) : 1;
   }
   const int T = bf ? 64 : 32;
@@ -533,7 +773,8 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   if (splits < 1) splits = 1;
   float* ws = splits > 1 ? (float*)a.workspace : nullptr;
 
-  if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
+  if (use_g8(a)) { if (cbf) dispatch_g8<bf16>(a, e, ws, splits, tps, s); else dispatch_g8<float>(a, e, ws, splits, tps, s); }
+  else if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
   else { if (cbf) dispatch_layout<float, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<float, float>(a, e, ws, splits, tps, s); }
   MMFD_CHECK_LAUNCH("gemm_mfma");
   if (ws) {
