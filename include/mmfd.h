@@ -81,10 +81,15 @@ typedef struct mmfd_gemm_args {
   mmfd_epilogue ep;
   void* workspace; int64_t workspace_bytes; /* split-K fp32 slabs; may be NULL (no split) */
   int splits;              /* 0 = choose automatically (bounded by workspace_bytes) */
+  /* optional fused row sums of op(A) (the bias gradient sum_tokens dY of a weight-gradient GEMM,
+     replacing the reference's autograd of nn.Linear.bias): a_rowsum[m] = a_rowsum_beta *
+     a_rowsum[m] + sum_k op(A)[m][k], fp32, M entries. NULL disables. */
+  float* a_rowsum; float a_rowsum_beta;
 } mmfd_gemm_args;
 
 int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);
-/* bytes of workspace the automatic split choice would like for this problem */
+/* bytes of workspace the automatic split choice would like for this problem (incl. the per-split
+   row-sum partials when a_rowsum is set) */
 int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* args);
 
 /* Column sums (bias gradients): out[n] = beta*out[n] + sum_m X[m*ldx + n]. workspace >= 4*N*256 B */

@@ -80,13 +80,33 @@ class StepCtx:
         return g, 1.0
 
     def lin_grads(self, names, dy2d, x2d):
-        """dW = dy^T x (fp32, accumulate), db = colsum(dy); `names` are the row blocks of dy."""
+        """dW = dy^T x (fp32, accumulate) with db = sum_rows(dy) fused into the same GEMM
+        (a_rowsum); `names` are the row blocks of dy. A packed group (fused QKV / K|V) whose
+        gradients are first written here is ONE GEMM into a packed buffer whose row blocks become
+        the parameters' gradient tensors."""
+        fresh = all(n + ".weight" not in self.grads and n + ".bias" not in self.grads for n in names)
+        has_b = all(n + ".bias" in self.P for n in names)
+        if len(names) > 1 and fresh and has_b:
+            rows = [self.P[n + ".weight"].shape[0] for n in names]
+            kin = self.P[names[0] + ".weight"].shape[1]
+            dev = self.P[names[0] + ".weight"].device
+            gw = torch.empty((sum(rows), kin), device=dev, dtype=torch.float32)
+            gb = torch.empty(sum(rows), device=dev, dtype=torch.float32)
+            K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=gw, a_rowsum=gb)
+            r = 0
+            for n, k in zip(names, rows):
+                self.grads[n + ".weight"] = gw[r:r + k]
+                self.grads[n + ".bias"] = gb[r:r + k]
+                r += k
+            return
         if len(names) == 1:
             n = names[0]
             g, beta = self.grad_slot(n + ".weight", self.P[n + ".weight"].shape)
-            K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta)
-            gb, bb = self.grad_slot(n + ".bias", self.P[n + ".bias"].shape)
-            K.colsum(dy2d, out=gb, beta=bb)
+            if n + ".bias" in self.P:
+                gb, bb = self.grad_slot(n + ".bias", self.P[n + ".bias"].shape)
+                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta, a_rowsum=gb, a_rowsum_beta=bb)
+            else:
+                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta)
             return
         r = 0
         for n in names:

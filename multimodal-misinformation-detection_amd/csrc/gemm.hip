@@ -414,11 +414,26 @@ __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2
   __builtin_amdgcn_s_setprio(0);
 }
 
+__device__ __forceinline__ float g8_sum8(uint4 x) {
+  return ((__uint_as_float(x.x << 16) + __uint_as_float(x.x & 0xffff0000u)) +
+          (__uint_as_float(x.y << 16) + __uint_as_float(x.y & 0xffff0000u))) +
+         ((__uint_as_float(x.z << 16) + __uint_as_float(x.z & 0xffff0000u)) +
+          (__uint_as_float(x.w << 16) + __uint_as_float(x.w & 0xffff0000u)));
+}
+// wave wc sums A subtile wc of the half-tile (its own two LDS reads: a runtime subtile index into
+// the fragment registers would push them to scratch)
+template <int LAYOUT>
+__device__ __forceinline__ float g8_rowsum(const char* img, int wr, int wc, int lane) {
+  return g8_sum8(load_frag<bf16, LAYOUT, 128>(img, wr * 4 + wc, 0, lane)) +
+         g8_sum8(load_frag<bf16, LAYOUT, 128>(img, wr * 4 + wc, 1, lane));
+}
+
 template <int TA, int TB, typename TC>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
-               float alpha, int tiles_per_split, EpiArgs e) {
+               float alpha, int tiles_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
+               int rs_mode) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -477,11 +492,17 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   g8_barrier();
   if (wr == 1) g8_barrier();  // stagger the second wave row by one barrier
 
+  // fused row sums of op(A) (bias gradient): blocks of the first column tile only; wave wc sums
+  // A subtile i == wc of each A fragment set it loads, lane (g, i) covering k-chunk g of row i
+  const bool do_rs = rs_mode != 0 && (tile % gx) == 0;
+  float rs0 = 0.f, rs1 = 0.f;
+
   uint4 fa[4][2], fb[2][2];
   for (int t = 0; t < nk; ++t) {
     // phase 0: quadrant (0,0)
     g8_frag_a<TA>(fa, img(t, 0), wr, lane);
     g8_frag_b<TB>(fb, img(t, 2), wc, lane);
+    if (do_rs) rs0 += g8_rowsum<TA>(img(t, 0), wr, wc, lane);
     if (t + 1 < nk) issue(2, t + 1);
     g8_pre_barrier();
     g8_mma(acc[0][0], fa, fb);
@@ -494,6 +515,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     g8_barrier();
     // phase 2: quadrant (1,1)
     g8_frag_a<TA>(fa, img(t, 1), wr, lane);
+    if (do_rs) rs1 += g8_rowsum<TA>(img(t, 1), wr, wc, lane);
     if (t + 2 < nk) issue(3, t + 2);
     g8_pre_barrier();
     g8_mma(acc[1][1], fa, fb);
@@ -513,6 +535,19 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   if (wr == 0) g8_barrier();  // re-align the wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (do_rs) {
+    rs0 += __shfl_xor(rs0, 16, 64);
+    rs0 += __shfl_xor(rs0, 32, 64);
+    rs1 += __shfl_xor(rs1, 16, 64);
+    rs1 += __shfl_xor(rs1, 32, 64);
+    if (lane < 16) {
+      float* dst = rs_mode == 1 ? rs_out : rs_out + (int64_t)blockIdx.z * M;
+      const float bt = rs_mode == 1 ? rs_beta : 0.f;
+      const int64_t r0 = m0 + wr * 64 + wc * 16 + lane, r1 = r0 + 128;
+      if (r0 < M) dst[r0] = (bt != 0.f ? bt * dst[r0] : 0.f) + rs0;
+      if (r1 < M) dst[r1] = (bt != 0.f ? bt * dst[r1] : 0.f) + rs1;
+    }
+  }
 
   // ---- epilogue: four passes of 64 rows (quadrant row mq = q >> 1 of wave row wr = q & 1)
   constexpr int LDC = G8_BN + 4;
@@ -625,7 +660,8 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
 }
 
 template <int TA, int TB, typename TC>
-void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s) {
+void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
+               int rs_mode, hipStream_t s) {
   dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<TA, TB, TC>),
@@ -633,15 +669,17 @@ void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits,
   }();
   (void)attr;
   hipLaunchKernelGGL((gemm256_kernel<TA, TB, TC>), grid, dim3(NT), G8_LDS, s, (const bf16*)a.A, a.lda,
-                     (const bf16*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e);
+                     (const bf16*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
+                     a.a_rowsum_beta, rs_mode);
 }
 
 template <typename TC>
-void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s) {
-  if (!a.trans_a && !a.trans_b) launch_g8<0, 0, TC>(a, e, ws, splits, tps, s);
-  else if (!a.trans_a && a.trans_b) launch_g8<0, 1, TC>(a, e, ws, splits, tps, s);
-  else if (a.trans_a && !a.trans_b) launch_g8<1, 0, TC>(a, e, ws, splits, tps, s);
-  else launch_g8<1, 1, TC>(a, e, ws, splits, tps, s);
+void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
+                 int rs_mode, hipStream_t s) {
+  if (!a.trans_a && !a.trans_b) launch_g8<0, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else if (!a.trans_a && a.trans_b) launch_g8<0, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else if (a.trans_a && !a.trans_b) launch_g8<1, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else launch_g8<1, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
 }
 
 bool use_g8(const mmfd_gemm_args& a) {
@@ -682,10 +720,15 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
     const int64_t tiles = ((a.M + G8_BM - 1) / G8_BM) * ((a.N + G8_BN - 1) / G8_BN);
     if (a.splits > 0) splits = a.splits;
     else if (nkt >= 16 && tiles < 256) {
+      // modelled time (us): rounds of 256 blocks x (K-tiles per block x ~1.8 us + ~3 us block
+      // overhead) + the fp32 slab round trip (written by the blocks, read by the reduce) at ~5 TB/s
       double best = 1e30;
       const int smax = (int)std::min<int64_t>(32, nkt / 8);
       for (int sp = 1; sp <= smax; ++sp) {
-        const double cost = (double)((tiles * sp + 255) / 256) / sp + (sp > 1 ? 0.05 : 0.0) + 0.004 * sp;
+        const double rounds = (double)((tiles * sp + 255) / 256);
+        const double kts = (double)((nkt + sp - 1) / sp);
+        double cost = rounds * (kts * 1.8 + 3.0);
+        if (sp > 1) cost += (double)sp * a.M * a.N * 8.0 / 5.0e6 + 4.0;
         if (cost < best) { best = cost; splits = sp; }
       }
     }
@@ -703,13 +746,31 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
   return splits;
 }
 
+// extra workspace for the fused row sums: per-split partials (G8) or the colsum partials (others)
+int64_t rowsum_ws_bytes(const mmfd_gemm_args& a, int splits, bool g8) {
+  if (!a.a_rowsum) return 0;
+  if (g8) return splits > 1 ? (int64_t)splits * a.M * 4 : 0;
+  const int64_t nparts = std::min<int64_t>(256, std::max<int64_t>(1, a.K / 64));
+  return nparts * a.M * 4;
+}
+
+// row sums of op(A) for the non-G8 paths: with trans_a, op(A) rows are the columns of the stored
+// [K][M] matrix, i.e. mmfd_colsum
+int rowsum_fallback(const mmfd_gemm_args& a, void* ws, int64_t ws_bytes, hipStream_t s) {
+  if (!a.a_rowsum) return 0;
+  if (!a.trans_a)
+    return mmfd_set_error(MMFD_ERR_UNSUPPORTED, "mmfd_gemm: a_rowsum without trans_a needs the bf16 MFMA path");
+  return mmfd_colsum(a.dtype, a.K, a.M, a.A, a.lda, a.a_rowsum, a.a_rowsum_beta, ws, ws_bytes, s);
+}
+
 }  // namespace
 
 extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
-  if (!a || !mfma_ok(*a)) return 0;
+  if (!a) return 0;
+  if (!mfma_ok(*a)) return rowsum_ws_bytes(*a, 1, false);
   int64_t need = 0;
-  choose_splits(*a, &need);
-  return need;
+  const int splits = choose_splits(*a, &need);
+  return need + rowsum_ws_bytes(*a, splits, use_g8(*a));
 }
 
 extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
@@ -755,14 +816,14 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     else { if (cbf) SIMPLE(float, bf16); else SIMPLE(float, float); }
 #undef SIMPLE
     MMFD_CHECK_LAUNCH("gemm_simple");
-    return 0;
+    return rowsum_fallback(a, a.workspace, a.workspace_bytes, s);
   }
 
   int64_t need = 0;
   int splits = choose_splits(a, &need);
-  if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need)) {
+  if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need + rowsum_ws_bytes(a, splits, use_g8(a)))) {
     // shrink to what the workspace allows
-    const int64_t per = a.M * a.N * 4;
+    const int64_t per = a.M * a.N * 4 + (a.a_rowsum ? a.M * 4 : 0);
     int fit = (a.workspace && per > 0) ? (int)std::min<int64_t>(a.workspace_bytes / per, 32) : 1;
     splits = fit > 1 ? std::min(splits, fit) : 1;
   }
@@ -772,8 +833,13 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   splits = tps > 0 ? (nkt + tps - 1) / tps : 1;
   if (splits < 1) splits = 1;
   float* ws = splits > 1 ? (float*)a.workspace : nullptr;
+  const bool g8 = use_g8(a);
+  // fused row sums: G8 writes them directly (one split) or as per-split partials after the slabs
+  float* rs_part = (a.a_rowsum && g8 && splits > 1) ? (float*)a.workspace + (int64_t)splits * a.M * a.N : nullptr;
+  const int rs_mode = (!a.a_rowsum || !g8) ? 0 : (splits > 1 ? 2 : 1);
+  float* rs_out = rs_mode == 2 ? rs_part : a.a_rowsum;
 
-  if (use_g8(a)) { if (cbf) dispatch_g8<bf16>(a, e, ws, splits, tps, s); else dispatch_g8<float>(a, e, ws, splits, tps, s); }
+  if (g8) { if (cbf) dispatch_g8<bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
   else if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
   else { if (cbf) dispatch_layout<float, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<float, float>(a, e, ws, splits, tps, s); }
   MMFD_CHECK_LAUNCH("gemm_mfma");
@@ -783,6 +849,15 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc, a.M, a.N, e);
     else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc, a.M, a.N, e);
     MMFD_CHECK_LAUNCH("splitk_reduce");
+  }
+  if (rs_mode == 2) {
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((a.M + 63) / 64)), dim3(1024), 0, s,
+                       (const float*)rs_part, splits, a.M, a.M, a.a_rowsum, a.a_rowsum_beta);
+    MMFD_CHECK_LAUNCH("gemm rowsum reduce");
+  } else if (a.a_rowsum && !g8) {
+    char* base = (char*)a.workspace + (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
+    const int64_t left = a.workspace_bytes - (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
+    return rowsum_fallback(a, base, left, s);
   }
   return 0;
 }

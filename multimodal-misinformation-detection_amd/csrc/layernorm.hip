@@ -163,6 +163,176 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, int width, co
   }
 }
 
+
+// ---- 16-byte vector variants (width a multiple of 8 bf16 / 4 fp32): one wave per row, lane owns
+// 16-B chunks c = lane + 64 j
+template <typename T> struct VN;
+template <> struct VN<float> {
+  static constexpr int N = 4, MAXV = 4;
+  __device__ __forceinline__ static void load(const float* p, float (&v)[N]) {
+    const float4 x = *reinterpret_cast<const float4*>(p); v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[N]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct VN<bf16> {
+  static constexpr int N = 8, MAXV = 2;
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[N]) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float (&v)[N]) {
+    bf16x8 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, o);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ void load_f32xN(const float* p, float (&v)[VN<T>::N]) {
+#pragma unroll
+  for (int i = 0; i < VN<T>::N; i += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p + i);
+    v[i] = a.x; v[i + 1] = a.y; v[i + 2] = a.z; v[i + 3] = a.w;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, const T* __restrict__ x, int64_t ldx,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, T* __restrict__ y, int64_t ldy,
+                                                       float* __restrict__ mean, float* __restrict__ rstd) {
+  constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = width / N;
+  float v[MAXV][N];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      VN<T>::load(x + row * ldx + N * c, v[j]);
+#pragma unroll
+      for (int e = 0; e < N; ++e) s += v[j][e];
+    }
+  }
+  const float mu = wave_sum(s) / (float)width;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch)
+#pragma unroll
+      for (int e = 0; e < N; ++e) { const float d = v[j][e] - mu; q += d * d; }
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)width + eps);
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      float gg[N], bb[N], o[N];
+      load_f32xN<T>(gamma + N * c, gg);
+      load_f32xN<T>(beta + N * c, bb);
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] = (v[j][e] - mu) * rs * gg[e] + bb[e];
+      VN<T>::store(y + row * ldy + N * c, o);
+    }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, const T* __restrict__ dy, int64_t lddy,
+                                                       const T* __restrict__ x, int64_t ldx, const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       T* __restrict__ dx, int64_t lddx, const T* __restrict__ dx_add,
+                                                       int64_t ldadd, T* __restrict__ dx_drop, float p, uint32_t thr,
+                                                       const uint64_t* __restrict__ seedp, uint64_t salt,
+                                                       float* __restrict__ part) {
+  constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
+  __shared__ float red[4][2][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = width / N;
+  const uint64_t seed = (dx_drop && p > 0.f) ? *seedp : 0ull;
+  const float keep = 1.0f / (1.0f - p);
+  float pg[MAXV][N], pb[MAXV][N];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+#pragma unroll
+    for (int e = 0; e < N; ++e) { pg[j][e] = 0.f; pb[j][e] = 0.f; }
+
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXV][N], g[MAXV][N], add[MAXV][N];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        float d[N], gv[N];
+        VN<T>::load(dy + row * lddy + N * c, d);
+        VN<T>::load(x + row * ldx + N * c, xh[j]);
+        if (dx_add) VN<T>::load(dx_add + row * ldadd + N * c, add[j]);
+        load_f32xN<T>(gamma + N * c, gv);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          xh[j][e] = (xh[j][e] - mu) * rs;
+          g[j][e] = d[e] * gv[e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+          pg[j][e] += d[e] * xh[j][e];
+          pb[j][e] += d[e];
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / (float)width;
+    const float c2 = wave_sum(s2) / (float)width;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        float o[N];
+#pragma unroll
+        for (int e = 0; e < N; ++e) o[e] = rs * (g[j][e] - c1 - xh[j][e] * c2) + (dx_add ? add[j][e] : 0.f);
+        VN<T>::store(dx + row * lddx + N * c, o);
+        if (dx_drop) {
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            const uint32_t h = mmfd_hash(seed, salt, (uint64_t)row * (uint64_t)width + N * c + e);
+            o[e] = (p > 0.f && h < thr) ? 0.f : o[e] * (p > 0.f ? keep : 1.f);
+          }
+          VN<T>::store(dx_drop + row * lddx + N * c, o);
+        }
+      }
+    }
+  }
+  // block reduction of the per-lane column partials, 64*N columns per slab
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    if (64 * j >= nch) break;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      red[wave][0][lane * N + e] = pg[j][e];
+      red[wave][1][lane * N + e] = pb[j][e];
+    }
+    __syncthreads();
+    for (int cl = threadIdx.x; cl < 64 * N; cl += 256) {
+      const int col = 64 * N * j + cl;
+      if (col < width) {
+        const float sg = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+        const float sb = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+        part[((int64_t)blockIdx.x * 2 + 0) * width + col] = sg;
+        part[((int64_t)blockIdx.x * 2 + 1) * width + col] = sb;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
@@ -173,7 +343,15 @@ extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const 
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
-  if (dtype == MMFD_BF16)
+  const int epc = dtype == MMFD_BF16 ? 8 : 4;
+  const bool v16 = width % epc == 0 && ldx % epc == 0 && ldy % epc == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0;
+  if (v16) {
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
+    else
+      hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+  } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
   else
     hipLaunchKernelGGL((ln_fwd_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
@@ -191,13 +369,27 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
   MMFD_CHECK_ARG(!(dx_drop && dropout_p > 0.f) || seed, "layernorm_bwd: dropout needs seed");
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  int nblocks = (int)std::min<int64_t>((rows + 3) / 4, 512);
+  int nblocks = (int)std::min<int64_t>((rows + 3) / 4, 2048);
   const int64_t per = 2 * width * 4;
   if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
   MMFD_CHECK_ARG(nblocks >= 1 && workspace, "layernorm_bwd: workspace too small");
   const float p = dropout_p > 0.f ? dropout_p : 0.f;
   const uint32_t thr = mmfd_drop_threshold(p);
-  if (dtype == MMFD_BF16)
+  const int epc = dtype == MMFD_BF16 ? 8 : 4;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const bool v16 = width % epc == 0 && lddy % epc == 0 && ldx % epc == 0 && lddx % epc == 0 &&
+                   (!dx_add || (ldadd % epc == 0 && al(dx_add))) && al(dy) && al(x) && al(dx) && al(gamma) &&
+                   (!dx_drop || al(dx_drop));
+  if (v16) {
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((ln_bwd16_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
+                         (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd,
+                         (bf16*)dx_drop, p, thr, seed, salt, (float*)workspace);
+    else
+      hipLaunchKernelGGL((ln_bwd16_kernel<float>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const float*)dy,
+                         lddy, (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx, (const float*)dx_add, ldadd,
+                         (float*)dx_drop, p, thr, seed, salt, (float*)workspace);
+  } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
                        (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd, (bf16*)dx_drop,
                        p, thr, seed, salt, (float*)workspace);

@@ -47,6 +47,7 @@ class GemmArgs(ctypes.Structure):
         ("ep", EpilogueArgs),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("splits", ctypes.c_int),
+        ("a_rowsum", ctypes.c_void_p), ("a_rowsum_beta", ctypes.c_float),
     ]
 
 
@@ -248,9 +249,11 @@ def _kernel_name(a, split):
 
 
 def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
-         residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0):
+         residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0, a_rowsum=None,
+         a_rowsum_beta=0.0):
     """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
-    nn.Linear weight) when trans_b=False, else B ([K,N] stored)."""
+    nn.Linear weight) when trans_b=False, else B ([K,N] stored). `a_rowsum` (fp32 [M]) additionally
+    receives a_rowsum_beta * a_rowsum + sum_k op(A)[m, k] (bias gradient of a weight-gradient GEMM)."""
     _require_cuda(A, B, out, bias, residual, aux)
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
@@ -293,6 +296,11 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
     a.ep.seed = seed.t.data_ptr() if seed is not None else None
     a.ep.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
     a.splits = int(splits)
+    if a_rowsum is not None:
+        if a_rowsum.dtype != torch.float32 or a_rowsum.numel() != M or not a_rowsum.is_contiguous():
+            raise ValueError("a_rowsum must be a contiguous fp32 vector of length M")
+        _require_cuda(a_rowsum)
+        a.a_rowsum, a.a_rowsum_beta = a_rowsum.data_ptr(), float(a_rowsum_beta)
     L = lib()
     need = L.mmfd_gemm_workspace_bytes(ctypes.byref(a))
     ws = None
@@ -423,7 +431,7 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None
     _require_cuda(dy, x, gamma, mean, rstd)
     R, W = dy.shape
     dx = dx if dx is not None else torch.empty((R, W), device=dy.device, dtype=dy.dtype)
-    nb = max(1, min((R + 3) // 4, 512))
+    nb = max(1, min((R + 3) // 4, 2048))
     ws = torch.empty(nb * 2 * W, device=dy.device, dtype=torch.float32)
     _check(lib().mmfd_layernorm_bwd(dtype_code(dy.dtype), R, W, _ptr(dy), _ld(dy), _ptr(x), _ld(x), _ptr(gamma),
                                     _ptr(mean), _ptr(rstd), _ptr(dx), _ld(dx), _ptr(dx_add),

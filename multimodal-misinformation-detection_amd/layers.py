@@ -48,8 +48,8 @@ class _LinearFn(torch.autograd.Function):
             dy2 = K.act_bwd(dy2, aux if act else dy2, K.ACT_GELU if act else K.ACT_NONE, dropout_p=p, seed=seed,
                             salt=K.salt_of(site))
         dx = K.gemm(dy2, wc, trans_b=True).reshape(shp) if ctx.needs_input_grad[0] else None
-        dw = K.gemm(dy2, x2, trans_a=True, trans_b=True, out_dtype=torch.float32)
-        db = K.colsum(dy2) if has_b else None
+        db = torch.empty(dy2.shape[1], device=dy2.device, dtype=torch.float32) if has_b else None
+        dw = K.gemm(dy2, x2, trans_a=True, trans_b=True, out_dtype=torch.float32, a_rowsum=db)
         return dx, dw, db, None, None, None, None
 
 

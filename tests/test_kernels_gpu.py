@@ -77,6 +77,35 @@ def test_gemm_splitk_long_k(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8192, 256, 384), (300, 768, 512), (4096, 2304, 768), (130, 40, 24), (64, 40, 36)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_fused_rowsum(dtype, shape, beta):
+    """dW = dY^T X with the bias gradient sum_tokens dY fused (split-K and direct, MFMA and
+    simple/unaligned paths); beta=1 accumulates like a shared parameter's second use."""
+    Kd, M, N = shape
+    A = _rand(Kd, M, dtype=dtype, seed=31); B = _rand(Kd, N, dtype=dtype, seed=32)
+    rs0 = _rand(M, seed=33)
+    rs = rs0.clone().to(DEV)
+    out = K.gemm(A.to(DEV), B.to(DEV), trans_a=True, trans_b=True, out_dtype=torch.float32, a_rowsum=rs,
+                 a_rowsum_beta=beta)
+    torch.cuda.synchronize()
+    ref = A.double().T @ B.double()
+    assert (out.double().cpu() - ref).abs().max().item() <= 2e-3 * max(1.0, math.sqrt(Kd / 1024))
+    rref = A.double().sum(0) + beta * rs0.double()
+    assert (rs.double().cpu() - rref).abs().max().item() <= 1e-4 * math.sqrt(Kd)
+
+
+def test_gemm_fused_rowsum_nontransposed_bf16():
+    """row sums of a K-contiguous A (layout 0) on the bf16 256x256 path"""
+    M, N, Kd = 512, 256, 640
+    A = _rand(M, Kd, dtype=torch.bfloat16, seed=34); B = _rand(N, Kd, dtype=torch.bfloat16, seed=35)
+    rs = torch.empty(M, device=DEV)
+    K.gemm(A.to(DEV), B.to(DEV), out_dtype=torch.float32, a_rowsum=rs)
+    torch.cuda.synchronize()
+    assert (rs.double().cpu() - A.double().sum(1)).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_epilogues(dtype):
     M, N, Kd = 300, 256, 128
     x = _rand(M, Kd, dtype=dtype, seed=5); w = _rand(N, Kd, dtype=dtype, seed=6, scale=0.1)
