@@ -68,6 +68,8 @@ typedef struct mmfd_epilogue {
   float dropout_p;         /* 0 disables */
   const uint64_t* seed;    /* device pointer to the step seed (read by the kernel) */
   uint64_t salt;           /* call-site id; element index = m * N + n */
+  int residual_first;      /* 1: z += residual BEFORE the (forward) activation, i.e. act(acc + bias +
+                              residual) — the ResNet bottleneck's relu(bn3(conv3) + identity) */
 } mmfd_epilogue;
 
 typedef struct mmfd_gemm_args {
@@ -174,12 +176,53 @@ int mmfd_embed_ln_fwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t*
                       const float* type, const float* gamma, const float* beta, float eps,
                       void* sum_out, void* y, float* mean, float* rstd, float dropout_p,
                       const uint64_t* seed, uint64_t salt, mmfd_stream_t stream);
+/* Generalised embeddings (HF MPNetEmbeddings / RoBERTa-style, text2text_retrieval.py:21,125 bi-encoder):
+   position_ids (NULL = 0..L-1 per sequence), token_type_ids/type (NULL = no type table),
+   sum_out/mean/rstd (NULL = not saved; inference). */
+int mmfd_embed_ln_fwd_ex(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                         const int64_t* position_ids, const int64_t* token_type_ids, const float* word,
+                         const float* pos, const float* type, const float* gamma, const float* beta, float eps,
+                         void* sum_out, void* y, float* mean, float* rstd, float dropout_p,
+                         const uint64_t* seed, uint64_t salt, mmfd_stream_t stream);
+/* position ids = padding_idx + running count of non-pad tokens (pads get padding_idx), int64 [B][L] */
+int mmfd_position_ids(int64_t B, int64_t L, const int64_t* input_ids, int64_t padding_idx, int64_t* out,
+                      mmfd_stream_t stream);
+/* relative position bias (MPNet encoder.relative_attention_bias): out[h][q][k] = table[bucket[q][k]][h];
+   bucket int32 [Lq][Lk] (host-computed with the reference's bucket formula), table fp32 [nb][H] */
+int mmfd_rel_bias(int64_t H, int64_t Lq, int64_t Lk, const int32_t* bucket, const float* table, float* out,
+                  mmfd_stream_t stream);
 /* scatter-add the gradient of the pre-LN sum into the three tables (fp32 atomics for word). */
 int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
                    const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos,
                    float* dtype_emb, int64_t padding_idx, mmfd_stream_t stream);
 /* key-padding mask (int64 0/1) -> additive bias (0 or `neg`, HF uses finfo(float32).min) */
 int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, float neg, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* ResNet50 evidence-image extractor (im2im_retrieval.py:14-36, torchvision resnet50 minus fc): */
+/* NHWC activations, convolutions as MFMA GEMMs (mmfd_gemm) over im2col gathers, eval-mode      */
+/* BatchNorm folded into the weights, ReLU / residual add in the GEMM epilogue.                 */
+/* ------------------------------------------------------------------------------------------- */
+/* out_w[co][(kh*KW+kw)*Cin+ci] = w[co][ci][kh][kw]*s[co] (zero for k >= KH*KW*Cin < Kpad),
+   out_b[co] = beta - mean*s, s = gamma/sqrt(var+eps); gamma == NULL: no BatchNorm (s=1, b=0) */
+int mmfd_conv_weight_prep(int dtype, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t Kpad,
+                          const float* w, const float* gamma, const float* beta, const float* mean,
+                          const float* var, float eps, void* out_w, float* out_b, mmfd_stream_t stream);
+/* NHWC im2col: out[(n*Ho+ho)*Wo+wo][(kh*KW+kw)*C+c] (zero outside the image and for k >= KH*KW*C);
+   C a multiple of 16 B; also the strided 1x1 gather of the downsample shortcut */
+int mmfd_im2col_nhwc(int dtype, int64_t N, int64_t H, int64_t W, int64_t C, int KH, int KW, int stride,
+                     int pad, int64_t Ho, int64_t Wo, int64_t Kpad, const void* x, void* out,
+                     mmfd_stream_t stream);
+/* stem im2col from fp32 NCHW pixels (same column order (kh, kw, c)) */
+int mmfd_im2col_nchw(int dtype, int64_t N, int64_t C, int64_t H, int64_t W, int KH, int KW, int stride,
+                     int pad, int64_t Ho, int64_t Wo, int64_t Kpad, const float* x, void* out,
+                     mmfd_stream_t stream);
+/* k x k max pooling on NHWC (nn.MaxPool2d(3, 2, 1)) */
+int mmfd_maxpool_nhwc(int dtype, int64_t N, int64_t H, int64_t W, int64_t C, int k, int stride, int pad,
+                      int64_t Ho, int64_t Wo, const void* x, void* out, mmfd_stream_t stream);
+/* global average pool NHWC [N][HW][C] -> fp32 [N][C] (nn.AdaptiveAvgPool2d(1) + flatten) */
+int mmfd_global_avgpool(int dtype, int64_t N, int64_t HW, int64_t C, const void* x, float* out,
+                        mmfd_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------- */
 /* ViT patch embedding support (HF ViTPatchEmbeddings conv16/s16 == GEMM over patches).         */

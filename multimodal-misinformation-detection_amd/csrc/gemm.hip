@@ -39,12 +39,14 @@ struct EpiArgs {
   const uint64_t* seed; uint64_t salt;
   float beta;
   int vec;  // host-checked: C / residual / aux 16-B aligned with leading dims multiple of 8
+  int res_first;  // residual added before the forward activation
 };
 
 template <typename TC>
 __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t ldc, int64_t N,
                                                int64_t row, int64_t col, float z, uint64_t seed) {
   if (e.bias) z += e.bias[col];
+  if (e.res_first && e.residual) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
   if (e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU) {
     if (e.aux) reinterpret_cast<TC*>(e.aux)[row * e.ldaux + col] = from_f32<TC>(z);
     z = (e.act == MMFD_ACT_GELU) ? gelu_f(z) : fmaxf(z, 0.0f);
@@ -57,7 +59,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
     const uint32_t h = mmfd_hash(seed, e.salt, (uint64_t)row * (uint64_t)N + (uint64_t)col);
     z = (h < e.thr) ? 0.0f : z * e.keep_scale;
   }
-  if (e.residual) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
+  if (e.residual && !e.res_first) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
   TC* cp = C + row * ldc + col;
   if (e.beta != 0.0f) z += e.beta * to_f32(*cp);
   *cp = from_f32<TC>(z);
@@ -95,6 +97,12 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
     const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col), b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
     z[0] += b0.x; z[1] += b0.y; z[2] += b0.z; z[3] += b0.w; z[4] += b1.x; z[5] += b1.y; z[6] += b1.z; z[7] += b1.w;
   }
+  if (e.res_first && e.residual) {
+    float r[8];
+    V8<TC>::load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] += r[q];
+  }
   if (e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU) {
     if (e.aux) V8<TC>::store(reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col, z);
     if (e.act == MMFD_ACT_GELU) {
@@ -120,7 +128,7 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
 #pragma unroll
     for (int q = 0; q < 8; ++q) z[q] = (mmfd_hash(seed, e.salt, base + q) < e.thr) ? 0.0f : z[q] * e.keep_scale;
   }
-  if (e.residual) {
+  if (e.residual && !e.res_first) {
     float r[8];
     V8<TC>::load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col, r);
 #pragma unroll
@@ -794,7 +802,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   e.bias = a.ep.bias; e.residual = a.ep.residual; e.ldr = a.ep.ldr; e.aux = a.ep.aux;
   e.ldaux = a.ep.ldaux; e.act = act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
   e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
-  e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta;
+  e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta; e.res_first = a.ep.residual_first ? 1 : 0;
   {
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     bool v = al(a.C) && (a.ldc % 8) == 0;

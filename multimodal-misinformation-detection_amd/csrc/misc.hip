@@ -86,6 +86,7 @@ __global__ void xent_kernel(int n_paths, int64_t B, int64_t C, XentPtrs ptrs, co
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) embed_ln_fwd_kernel(int64_t B, int64_t L, int64_t D, const int64_t* __restrict__ ids,
+                                                           const int64_t* __restrict__ pos_ids,
                                                            const int64_t* __restrict__ tts, const float* __restrict__ word,
                                                            const float* __restrict__ pos, const float* __restrict__ type,
                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(256) embed_ln_fwd_kernel(int64_t B, int64_t L,
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B * L) return;
-  const int64_t t = row % L;
+  const int64_t t = pos_ids ? pos_ids[row] : row % L;
   const int64_t id = ids[row];
   const int64_t tt = tts ? tts[row] : 0;
   constexpr int MAXV = 16;  // D <= 1024
@@ -106,9 +107,12 @@ __global__ void __launch_bounds__(256) embed_ln_fwd_kernel(int64_t B, int64_t L,
     const int64_t d = lane + 64 * j;
     v[j] = 0.f;
     if (d < D) {
-      float e = word[id * D + d] + pos[t * D + d] + type[tt * D + d];
-      e = to_f32(from_f32<T>(e));  // the stored sum is what the backward LayerNorm re-reads
-      sum_out[row * D + d] = from_f32<T>(e);
+      float e = word[id * D + d] + pos[t * D + d];
+      if (type) e += type[tt * D + d];
+      if (sum_out) {
+        e = to_f32(from_f32<T>(e));  // the stored sum is what the backward LayerNorm re-reads
+        sum_out[row * D + d] = from_f32<T>(e);
+      }
       v[j] = e;
       s += e;
     }
@@ -135,7 +139,31 @@ __global__ void __launch_bounds__(256) embed_ln_fwd_kernel(int64_t B, int64_t L,
       y[row * D + d] = from_f32<T>(o);
     }
   }
-  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// MPNet/RoBERTa position ids: padding_idx + cumsum(id != padding_idx) on non-pad tokens, else
+// padding_idx (HF create_position_ids_from_input_ids). One thread per sequence.
+__global__ void position_ids_kernel(int64_t B, int64_t L, const int64_t* __restrict__ ids, int64_t padding_idx,
+                                    int64_t* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int64_t c = 0;
+  for (int64_t t = 0; t < L; ++t) {
+    const bool tok = ids[b * L + t] != padding_idx;
+    c += tok ? 1 : 0;
+    out[b * L + t] = (tok ? c : 0) + padding_idx;
+  }
+}
+
+// relative position bias out[h][q][k] = table[bucket[q][k]][h]
+__global__ void rel_bias_kernel(int64_t H, int64_t Lq, int64_t Lk, const int32_t* __restrict__ bucket,
+                                const float* __restrict__ table, float* __restrict__ out) {
+  const int64_t n = H * Lq * Lk;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t h = i / (Lq * Lk), qk = i % (Lq * Lk);
+    out[i] = table[(int64_t)bucket[qk] * H + h];
+  }
 }
 
 template <typename T>
@@ -295,24 +323,55 @@ extern "C" int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float*
   return 0;
 }
 
-extern "C" int mmfd_embed_ln_fwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
-                                 const int64_t* token_type_ids, const float* word, const float* pos, const float* type,
-                                 const float* gamma, const float* beta, float eps, void* sum_out, void* y, float* mean,
-                                 float* rstd, float dropout_p, const uint64_t* seed, uint64_t salt, mmfd_stream_t stream) {
+extern "C" int mmfd_embed_ln_fwd_ex(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                                    const int64_t* position_ids, const int64_t* token_type_ids, const float* word,
+                                    const float* pos, const float* type, const float* gamma, const float* beta, float eps,
+                                    void* sum_out, void* y, float* mean, float* rstd, float dropout_p,
+                                    const uint64_t* seed, uint64_t salt, mmfd_stream_t stream) {
   MMFD_CHECK_ARG(D <= 1024, "embed: D <= 1024");
   MMFD_CHECK_ARG(dropout_p <= 0.f || seed, "embed: dropout needs seed");
+  MMFD_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "embed: mean and rstd go together");
   const int64_t rows = B * L;
   if (rows == 0) return 0;
   const float p = dropout_p > 0.f ? dropout_p : 0.f;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == MMFD_BF16)
-    hipLaunchKernelGGL((embed_ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, B, L, D, input_ids, token_type_ids, word, pos, type,
-                       gamma, beta, eps, (bf16*)sum_out, (bf16*)y, mean, rstd, p, mmfd_drop_threshold(p), seed, salt);
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, B, L, D, input_ids, position_ids, token_type_ids,
+                       word, pos, type, gamma, beta, eps, (bf16*)sum_out, (bf16*)y, mean, rstd, p, mmfd_drop_threshold(p),
+                       seed, salt);
   else
-    hipLaunchKernelGGL((embed_ln_fwd_kernel<float>), grid, dim3(256), 0, s, B, L, D, input_ids, token_type_ids, word, pos, type,
-                       gamma, beta, eps, (float*)sum_out, (float*)y, mean, rstd, p, mmfd_drop_threshold(p), seed, salt);
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<float>), grid, dim3(256), 0, s, B, L, D, input_ids, position_ids, token_type_ids,
+                       word, pos, type, gamma, beta, eps, (float*)sum_out, (float*)y, mean, rstd, p, mmfd_drop_threshold(p),
+                       seed, salt);
   MMFD_CHECK_LAUNCH("embed_ln_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_embed_ln_fwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                                 const int64_t* token_type_ids, const float* word, const float* pos, const float* type,
+                                 const float* gamma, const float* beta, float eps, void* sum_out, void* y, float* mean,
+                                 float* rstd, float dropout_p, const uint64_t* seed, uint64_t salt, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(sum_out && mean && rstd && type, "embed_ln_fwd: sum_out/mean/rstd/type required (see _ex)");
+  return mmfd_embed_ln_fwd_ex(dtype, B, L, D, input_ids, nullptr, token_type_ids, word, pos, type, gamma, beta, eps,
+                              sum_out, y, mean, rstd, dropout_p, seed, salt, stream);
+}
+
+extern "C" int mmfd_position_ids(int64_t B, int64_t L, const int64_t* input_ids, int64_t padding_idx, int64_t* out,
+                                 mmfd_stream_t stream) {
+  if (B * L == 0) return 0;
+  hipLaunchKernelGGL(position_ids_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B, L,
+                     input_ids, padding_idx, out);
+  MMFD_CHECK_LAUNCH("position_ids");
+  return 0;
+}
+
+extern "C" int mmfd_rel_bias(int64_t H, int64_t Lq, int64_t Lk, const int32_t* bucket, const float* table, float* out,
+                             mmfd_stream_t stream) {
+  const int64_t n = H * Lq * Lk;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rel_bias_kernel, dim3(gridn(n, 256)), dim3(256), 0, (hipStream_t)stream, H, Lq, Lk, bucket, table, out);
+  MMFD_CHECK_LAUNCH("rel_bias");
   return 0;
 }
 

@@ -384,3 +384,134 @@ class _ViTFn(torch.autograd.Function):
         grads = [sc.grads.get(n) for n in fctx.names]
         fctx.sc = fctx.st = None
         return (None, None, None, None, *grads)
+
+
+# -------------------------------------------------------------------------------------------------
+# MPNet (the bi-encoder of the evidence corpus: SentenceTransformer("multi-qa-mpnet-base-dot-v1"),
+# text2text_retrieval.py:21,125,129-157) — inference only
+# -------------------------------------------------------------------------------------------------
+@dataclass
+class MPNetConfig:
+    vocab_size: int = 30527
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    max_position_embeddings: int = 514
+    layer_norm_eps: float = 1e-5
+    relative_attention_num_buckets: int = 32
+    pad_token_id: int = 1
+
+
+def mpnet_relative_buckets(L, num_buckets=32, max_distance=128):
+    """HF MPNetEncoder.relative_position_bucket over arange positions (host, int32 [L, L]); the bucket
+    map is a function of L only, computed once per length with the reference's float formula."""
+    import math
+    ctx_pos = torch.arange(L, dtype=torch.long)[:, None]
+    mem_pos = torch.arange(L, dtype=torch.long)[None, :]
+    n = -(mem_pos - ctx_pos)
+    nb = num_buckets // 2
+    ret = (n < 0).to(torch.long) * nb
+    n = torch.abs(n)
+    max_exact = nb // 2
+    is_small = n < max_exact
+    large = max_exact + (torch.log(n.float() / max_exact) / math.log(max_distance / max_exact)
+                         * (nb - max_exact)).to(torch.long)
+    large = torch.min(large, torch.full_like(large, nb - 1))
+    ret = ret + torch.where(is_small, n, large)
+    return ret.to(torch.int32)
+
+
+class MPNetModel(nn.Module):
+    """HF MPNetModel (add_pooling_layer=False) parameter layout; forward(input_ids, attention_mask)
+    returns .last_hidden_state. Inference only (the corpus extractor never trains it)."""
+
+    def __init__(self, config: MPNetConfig | None = None, **kw):
+        super().__init__()
+        c = config or MPNetConfig(**kw)
+        self.config = c
+        D = c.hidden_size
+        self.embeddings = nn.Module()
+        self.embeddings.word_embeddings = nn.Embedding(c.vocab_size, D, padding_idx=c.pad_token_id)
+        self.embeddings.position_embeddings = nn.Embedding(c.max_position_embeddings, D, padding_idx=c.pad_token_id)
+        self.embeddings.LayerNorm = nn.LayerNorm(D, eps=c.layer_norm_eps)
+        self.encoder = nn.Module()
+        self.encoder.layer = nn.ModuleList()
+        for _ in range(c.num_hidden_layers):
+            L = nn.Module()
+            L.attention = nn.Module()
+            L.attention.attn = nn.Module()
+            for n in ("q", "k", "v", "o"):
+                setattr(L.attention.attn, n, nn.Linear(D, D))
+            L.attention.LayerNorm = nn.LayerNorm(D, eps=c.layer_norm_eps)
+            L.intermediate = nn.Module()
+            L.intermediate.dense = nn.Linear(D, c.intermediate_size)
+            L.output = nn.Module()
+            L.output.dense = nn.Linear(c.intermediate_size, D)
+            L.output.LayerNorm = nn.LayerNorm(D, eps=c.layer_norm_eps)
+            self.encoder.layer.append(L)
+        self.encoder.relative_attention_bias = nn.Embedding(c.relative_attention_num_buckets, c.num_attention_heads)
+        self.compute_dtype = torch.float32
+        self._buckets = {}
+        self._init_weights()
+
+    def _init_weights(self, std=0.02):
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, 0.0, std)
+                if isinstance(m, nn.Linear) and m.bias is not None:
+                    nn.init.zeros_(m.bias)
+                if isinstance(m, nn.Embedding) and m.padding_idx is not None:
+                    with torch.no_grad():
+                        m.weight[m.padding_idx].zero_()
+            elif isinstance(m, nn.LayerNorm):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def set_precision(self, precision):
+        self.compute_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+        return self
+
+    def _bucket(self, L, dev):
+        key = (L, str(dev))
+        b = self._buckets.get(key)
+        if b is None:
+            b = self._buckets[key] = mpnet_relative_buckets(L, self.config.relative_attention_num_buckets).to(dev)
+        return b
+
+    @torch.no_grad()
+    def forward(self, input_ids, attention_mask=None, **unused):
+        params = dict(self.named_parameters())
+        dev = next(iter(params.values())).device
+        if dev.type != "cuda":
+            raise RuntimeError("mmfd MPNetModel runs on the HIP device: call .to('cuda') first")
+        P = {n: p.detach() for n, p in params.items()}
+        sc = Bk.StepCtx(P, self.compute_dtype)
+        ids = input_ids.to(dev).long().contiguous()
+        mask = attention_mask.to(dev).long().contiguous() if attention_mask is not None else None
+        out = mpnet_forward(sc, self.config, ids, mask, self._bucket(ids.shape[1], dev))
+        return EncoderOutput(last_hidden_state=out)
+
+
+def mpnet_forward(ctx: Bk.StepCtx, cfg: MPNetConfig, ids, mask, bucket):
+    B, L = ids.shape
+    D, H = cfg.hidden_size, cfg.num_attention_heads
+    eps = cfg.layer_norm_eps
+    P = ctx.P
+    pos_ids = K.position_ids(ids, cfg.pad_token_id)
+    x = K.embed_ln_infer(ids, pos_ids, P["embeddings.word_embeddings.weight"],
+                         P["embeddings.position_embeddings.weight"], P["embeddings.LayerNorm.weight"],
+                         P["embeddings.LayerNorm.bias"], eps, ctx.dt)
+    kb = K.mask_to_bias(mask) if mask is not None else None
+    rb = K.rel_bias(bucket, P["encoder.relative_attention_bias.weight"])
+    for i in range(cfg.num_hidden_layers):
+        p = f"encoder.layer.{i}"
+        qkv = Bk.linear_packed(ctx, x, [p + ".attention.attn.q", p + ".attention.attn.k",
+                                        p + ".attention.attn.v"]).view(B, L, 3 * D)
+        o, _ = K.attn_fwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], H, key_bias=kb, rel_bias=rb)
+        s1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.attn.o", residual=x)
+        h1, _, _ = Bk.layernorm(ctx, s1, p + ".attention.LayerNorm", eps)
+        f, _ = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU)
+        s2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=h1)
+        x, _, _ = Bk.layernorm(ctx, s2, p + ".output.LayerNorm", eps)
+    return x.view(B, L, D)

@@ -1,0 +1,304 @@
+"""Batched evidence-corpus embedding extractors on HIP kernels.
+
+a12  ResNet50 image features — the reference's `ImageSimilarity` (im2im_retrieval.py:12-42):
+     torchvision resnet50 with the classifier dropped (:14-17), eval mode, Resize(224) ->
+     ToTensor -> Normalize(ImageNet) (:19-27), one image per forward (:29-36), and `ImageCorpus`
+     (:45-78) looping over a directory. Here: NHWC bf16/fp32 activations, every convolution an MFMA
+     GEMM (1x1 convs read the activation directly, 3x3 / strided / stem convs via an im2col
+     gather), eval BatchNorm folded into the GEMM weights, ReLU and the bottleneck residual add in
+     the GEMM epilogue, global average pool into fp32 features; images are processed in batches.
+a13  MPNet sentence embeddings — the reference's `TextCorpus.encode_corpus` (text2text_retrieval.py:
+     125-157) through SentenceTransformer("multi-qa-mpnet-base-dot-v1") = MPNetModel + CLS pooling
+     (the model card's pooling; no normalisation) stored as fp16 with string ids (:144-154).
+
+Pretrained checkpoints cannot be downloaded here: models are randomly initialised unless a
+state_dict is given (torchvision / HF names load unchanged).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .encoders import MPNetConfig, MPNetModel
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+# -------------------------------------------------------------------------------------------------
+# ResNet50 (torchvision layout and parameter names)
+# -------------------------------------------------------------------------------------------------
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=False):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.stride = stride
+        if downsample:
+            self.downsample = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False),
+                                            nn.BatchNorm2d(planes * 4))
+        else:
+            self.downsample = None
+
+
+class ResNet(nn.Module):
+    """torchvision ResNet with Bottleneck blocks (resnet50: depths (3, 4, 6, 3), width 64).
+    forward(x [N, 3, H, W] fp32, normalised) -> [N, 2048, 1, 1], i.e. the reference's
+    nn.Sequential(*list(resnet50.children())[:-1]) (im2im_retrieval.py:15-17)."""
+
+    def __init__(self, depths=(3, 4, 6, 3), width=64, num_classes=1000):
+        super().__init__()
+        self.depths, self.width = tuple(depths), width
+        self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        inplanes = width
+        for i, d in enumerate(depths):
+            planes = width * (2 ** i)
+            stride = 1 if i == 0 else 2
+            blocks = [Bottleneck(inplanes, planes, stride, downsample=(stride != 1 or inplanes != planes * 4))]
+            inplanes = planes * 4
+            blocks += [Bottleneck(inplanes, planes) for _ in range(1, d)]
+            setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(inplanes, num_classes)  # unused by the extractor; kept for state_dict parity
+        self.out_features = inplanes
+        self.compute_dtype = torch.float32
+        self._prep = None
+        self._prep_key = None
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        self.eval()
+
+    def set_precision(self, precision):
+        self.compute_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+        self._prep = None
+        return self
+
+    # ---- folded GEMM weights (recomputed when any parameter/buffer changes) --------------------
+    def _prepared(self):
+        tensors = list(self.parameters()) + list(self.buffers())
+        key = (self.compute_dtype, tuple((t.data_ptr(), t._version) for t in tensors))
+        if self._prep is not None and self._prep_key == key:
+            return self._prep
+        dt = self.compute_dtype
+
+        def fold(conv, bn, kpad=None):
+            w = conv.weight.detach().float().contiguous()
+            return K.conv_weight_prep(w, dt, Kpad=kpad, eps=bn.eps,
+                                      bn=(bn.weight.detach().float().contiguous(), bn.bias.detach().float().contiguous(),
+                                          bn.running_mean.float().contiguous(), bn.running_var.float().contiguous()))
+
+        prep = {"stem": fold(self.conv1, self.bn1, kpad=_round_up(7 * 7 * 3, 8)), "blocks": []}
+        for i in range(len(self.depths)):
+            for blk in getattr(self, f"layer{i + 1}"):
+                prep["blocks"].append(dict(
+                    c1=fold(blk.conv1, blk.bn1), c2=fold(blk.conv2, blk.bn2), c3=fold(blk.conv3, blk.bn3),
+                    ds=fold(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None,
+                    stride=blk.stride, planes=blk.conv1.out_channels, cin=blk.conv1.in_channels))
+        self._prep, self._prep_key = prep, key
+        return prep
+
+    @torch.no_grad()
+    def forward(self, x):
+        dev = self.conv1.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("mmfd ResNet runs on the HIP device: call .to('cuda') first")
+        x = x.to(dev, torch.float32).contiguous()
+        N = x.shape[0]
+        prep = self._prepared()
+        dt = self.compute_dtype
+        w, b = prep["stem"]
+        cols, H, W = K.im2col_nchw(x, 7, 2, 3, w.shape[1], dt)
+        y = K.gemm(cols, w, bias=b, act=K.ACT_RELU)
+        del cols
+        y, H, W = K.maxpool_nhwc(y, N, H, W, self.width)
+        for blk in prep["blocks"]:
+            y, H, W = _bottleneck(y, N, H, W, blk)
+        feats = K.global_avgpool(y, N, H * W, y.shape[1])
+        return feats.view(N, -1, 1, 1)
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def _bottleneck(x, N, H, W, blk):
+    """relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + shortcut(x)) on NHWC rows"""
+    s, planes, cin = blk["stride"], blk["planes"], blk["cin"]
+    w1, b1 = blk["c1"]
+    h1 = K.gemm(x, w1, bias=b1, act=K.ACT_RELU)                          # 1x1
+    cols, Ho, Wo = K.im2col_nhwc(h1, N, H, W, planes, 3, s, 1)
+    del h1
+    w2, b2 = blk["c2"]
+    h2 = K.gemm(cols, w2, bias=b2, act=K.ACT_RELU)                       # 3x3 (stride s)
+    del cols
+    if blk["ds"] is not None:
+        wd, bd = blk["ds"]
+        src = x if s == 1 else K.im2col_nhwc(x, N, H, W, cin, 1, s, 0)[0]
+        ident = K.gemm(src, wd, bias=bd)                                  # 1x1 (stride s) + BN
+    else:
+        ident = x
+    w3, b3 = blk["c3"]
+    y = K.gemm(h2, w3, bias=b3, act=K.ACT_RELU, residual=ident, residual_first=True)
+    return y, Ho, Wo
+
+
+def resnet50(**kw):
+    return ResNet((3, 4, 6, 3), 64, **kw)
+
+
+# -------------------------------------------------------------------------------------------------
+# image preprocessing (im2im_retrieval.py:19-27) and the extractor API
+# -------------------------------------------------------------------------------------------------
+def preprocess(image, size=224):
+    """PIL image (or path / stream) -> fp32 [3, size, size]: Resize((size, size)) bilinear ->
+    ToTensor -> Normalize(ImageNet mean/std). Host side (as torchvision does on PIL images)."""
+    from PIL import Image
+    if not isinstance(image, Image.Image):
+        image = Image.open(image)
+    image = image.convert("RGB").resize((size, size), Image.BILINEAR)
+    a = np.asarray(image, dtype=np.float32) / 255.0
+    a = (a - np.asarray(IMAGENET_MEAN, np.float32)) / np.asarray(IMAGENET_STD, np.float32)
+    return torch.from_numpy(a.transpose(2, 0, 1).copy())
+
+
+class ImageSimilarity:
+    """im2im_retrieval.py:12-42 — ResNet50 features of one image (`extract_features`) plus the
+    batched `extract_batch` the corpus build uses."""
+
+    def __init__(self, state_dict=None, device="cuda", precision="bf16", model=None):
+        self.model = model if model is not None else resnet50()
+        if state_dict is not None:
+            self.model.load_state_dict(state_dict, strict=False)
+        self.model = self.model.to(device).eval().set_precision(precision)
+        self.device = device
+
+    def extract_batch(self, pixels):
+        """normalised fp32 [N, 3, 224, 224] (host or device) -> fp32 [N, 2048] on the device"""
+        return self.model(pixels).flatten(1)
+
+    def extract_features(self, image_stream):
+        x = preprocess(image_stream).unsqueeze(0)
+        return self.extract_batch(x).flatten().cpu()
+
+    @staticmethod
+    def similarity(features1, features2):
+        f1, f2 = features1.double().flatten(), features2.double().flatten()
+        den = max(float(f1.norm() * f2.norm()), 1e-6)  # nn.CosineSimilarity(dim=1, eps=1e-6)
+        return float((f1 @ f2) / den)
+
+
+class ImageCorpus:
+    """im2im_retrieval.py:45-78 with batched extraction. Features persist as an .npz archive
+    (`paths`, `features` [N, 2048] fp32) instead of a pickle."""
+
+    def __init__(self, feature_corpus_path, extractor: ImageSimilarity | None = None, batch_size=256):
+        self.feature_corpus_path = feature_corpus_path
+        self.feature_extractor = extractor or ImageSimilarity()
+        self.batch_size = batch_size
+        self.feature_dict = self.load_features()
+
+    def load_features(self):
+        if not os.path.exists(self.feature_corpus_path):
+            return {}
+        z = np.load(self.feature_corpus_path, allow_pickle=False)
+        return {p: torch.from_numpy(f) for p, f in zip(z["paths"].tolist(), z["features"])}
+
+    def save_features(self):
+        paths = list(self.feature_dict)
+        feats = np.stack([self.feature_dict[p].numpy() for p in paths]) if paths else np.zeros((0, 2048), np.float32)
+        with open(self.feature_corpus_path, "wb") as f:
+            np.savez(f, paths=np.array(paths), features=feats)
+
+    def add_image(self, image_path):
+        self.feature_dict[image_path] = self.feature_extractor.extract_features(image_path)
+        self.save_features()
+
+    def create_feature_corpus(self, image_dir):
+        paths = [os.path.join(image_dir, n) for n in sorted(os.listdir(image_dir))]
+        paths = [p for p in paths if os.path.isfile(p) and p.lower().endswith((".png", ".jpg", ".jpeg"))]
+        for i in range(0, len(paths), self.batch_size):
+            chunk = paths[i:i + self.batch_size]
+            px = torch.stack([preprocess(p) for p in chunk])
+            feats = self.feature_extractor.extract_batch(px).cpu()
+            for p, f in zip(chunk, feats):
+                self.feature_dict[p] = f
+        self.save_features()
+
+
+# -------------------------------------------------------------------------------------------------
+# text corpus (text2text_retrieval.py:123-157)
+# -------------------------------------------------------------------------------------------------
+class SentenceEncoder:
+    """MPNet + CLS pooling (SentenceTransformer("multi-qa-mpnet-base-dot-v1").encode semantics on
+    token ids). `encode(texts)` needs a tokenizer object (none can be downloaded here)."""
+
+    def __init__(self, model: MPNetModel | None = None, state_dict=None, device="cuda", precision="bf16",
+                 tokenizer=None, max_seq_length=512):
+        self.model = model if model is not None else MPNetModel(MPNetConfig())
+        if state_dict is not None:
+            self.model.load_state_dict(state_dict, strict=False)
+        self.model = self.model.to(device).eval().set_precision(precision)
+        self.tokenizer = tokenizer
+        self.max_seq_length = max_seq_length
+
+    def encode_ids(self, input_ids, attention_mask=None, batch_size=256):
+        """int64 [N, L] -> fp32 [N, 768] CLS embeddings (device)"""
+        outs = []
+        for i in range(0, input_ids.shape[0], batch_size):
+            ids = input_ids[i:i + batch_size]
+            m = attention_mask[i:i + batch_size] if attention_mask is not None else None
+            h = self.model(input_ids=ids, attention_mask=m).last_hidden_state
+            outs.append(K.cast(h[:, 0].contiguous(), torch.float32))
+        return torch.cat(outs) if len(outs) > 1 else outs[0]
+
+    def encode(self, sentences, batch_size=256, convert_to_tensor=True):
+        if self.tokenizer is None:
+            raise RuntimeError("SentenceEncoder.encode needs a tokenizer (pass tokenizer=...); use encode_ids")
+        enc = self.tokenizer(list(sentences), padding=True, truncation=True, max_length=self.max_seq_length,
+                             return_tensors="pt")
+        emb = self.encode_ids(enc["input_ids"], enc["attention_mask"], batch_size).cpu()
+        return emb if convert_to_tensor else emb.numpy()
+
+
+class TextCorpus:
+    """text2text_retrieval.py:123-157: encode `{split}_enriched.csv`'s evidence_enriched column and
+    store fp16 embeddings with ids `{split}_{id}` (HDF5 when h5py is importable, else .npz)."""
+
+    def __init__(self, data_dir, split, encoder: SentenceEncoder | None = None, out_dir=None):
+        self.bi_encoder = encoder or SentenceEncoder()
+        self.split, self.data_dir = split, data_dir
+        self.out_dir = out_dir or data_dir
+
+    def encode_corpus(self):
+        import pandas as pd
+        df = pd.read_csv(os.path.join(self.data_dir, f"{self.split}_enriched.csv"))
+        emb = self.bi_encoder.encode(df["evidence_enriched"].tolist()).numpy().astype(np.float16)
+        ids = [f"{self.split}_{i}" for i in df["id"].tolist()]
+        try:
+            import h5py
+            path = os.path.join(self.out_dir, f"{self.split}_embeddings.h5")
+            with h5py.File(path, "w") as h5:
+                h5.create_dataset("embeddings", data=emb, dtype="float16")
+                h5.create_dataset("ids", data=ids, dtype=h5py.string_dtype())
+        except ImportError:
+            path = os.path.join(self.out_dir, f"{self.split}_embeddings.npz")
+            np.savez(path, embeddings=emb, ids=np.array(ids))
+        return path

@@ -33,6 +33,7 @@ class EpilogueArgs(ctypes.Structure):
         ("dropout_p", ctypes.c_float),
         ("seed", ctypes.c_void_p),
         ("salt", ctypes.c_uint64),
+        ("residual_first", ctypes.c_int),
     ]
 
 
@@ -106,6 +107,15 @@ SIGNATURES = {
                                _F, _VP, _U64, _VP]),
     "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     "mmfd_mask_to_bias": (_I, [_I64, _VP, _VP, _F, _VP]),
+    "mmfd_embed_ln_fwd_ex": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
+                                  _F, _VP, _U64, _VP]),
+    "mmfd_position_ids": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
+    "mmfd_conv_weight_prep": (_I, [_I, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP]),
+    "mmfd_im2col_nhwc": (_I, [_I, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _I64, _I64, _I64, _VP, _VP, _VP]),
+    "mmfd_im2col_nchw": (_I, [_I, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _I64, _I64, _I64, _VP, _VP, _VP]),
+    "mmfd_maxpool_nhwc": (_I, [_I, _I64, _I64, _I64, _I64, _I, _I, _I, _I64, _I64, _VP, _VP, _VP]),
+    "mmfd_global_avgpool": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP]),
+    "mmfd_rel_bias": (_I, [_I64, _I64, _I64, _VP, _VP, _VP, _VP]),
     "mmfd_patchify": (_I, [_I, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _VP]),
     "mmfd_vit_tokens_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
     "mmfd_vit_tokens_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
@@ -250,7 +260,7 @@ def _kernel_name(a, split):
 
 def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
          residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0, a_rowsum=None,
-         a_rowsum_beta=0.0):
+         a_rowsum_beta=0.0, residual_first=False):
     """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
     nn.Linear weight) when trans_b=False, else B ([K,N] stored). `a_rowsum` (fp32 [M]) additionally
     receives a_rowsum_beta * a_rowsum + sum_k op(A)[m, k] (bias gradient of a weight-gradient GEMM)."""
@@ -289,6 +299,7 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
     a.ep.bias = bias.data_ptr() if bias is not None else None
     if residual is not None:
         a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
+        a.ep.residual_first = int(bool(residual_first))
     if aux is not None:
         a.ep.aux, a.ep.ldaux = aux.data_ptr(), _ld(aux)
     a.ep.act = int(act)
@@ -533,6 +544,86 @@ def embed_ln_fwd(ids, tts, word, pos, typ, gamma, beta, eps, dtype, dropout_p=0.
                                    _ptr(rstd), float(dropout_p), seed.ptr() if seed is not None else None,
                                    int(salt) & 0xFFFFFFFFFFFFFFFF, _stream()), "mmfd_embed_ln_fwd")
     return s, y, mean, rstd
+
+
+def embed_ln_infer(ids, pos_ids, word, pos, gamma, beta, eps, dtype, tts=None, typ=None):
+    """inference embeddings: y = LN(word[id] + pos[pos_id] (+ type[tt])), nothing saved"""
+    B, L = ids.shape
+    D = word.shape[1]
+    y = torch.empty((B * L, D), device=ids.device, dtype=dtype)
+    _check(lib().mmfd_embed_ln_fwd_ex(dtype_code(dtype), B, L, D, _ptr(ids.contiguous()),
+                                      _ptr(pos_ids.contiguous()) if pos_ids is not None else None,
+                                      _ptr(tts.contiguous()) if tts is not None else None, _ptr(word), _ptr(pos),
+                                      _ptr(typ) if typ is not None else None, _ptr(gamma), _ptr(beta), float(eps),
+                                      None, _ptr(y), None, None, 0.0, None, 0, _stream()), "mmfd_embed_ln_fwd_ex")
+    return y
+
+
+def position_ids(ids, padding_idx):
+    ids = ids.contiguous()
+    out = torch.empty_like(ids)
+    _check(lib().mmfd_position_ids(ids.shape[0], ids.shape[1], _ptr(ids), int(padding_idx), _ptr(out), _stream()),
+           "mmfd_position_ids")
+    return out
+
+
+def rel_bias(bucket, table):
+    """bucket int32 [Lq, Lk] (device), table fp32 [nb, H] -> fp32 [H, Lq, Lk]"""
+    Lq, Lk = bucket.shape
+    H = table.shape[1]
+    out = torch.empty((H, Lq, Lk), device=table.device, dtype=torch.float32)
+    _check(lib().mmfd_rel_bias(H, Lq, Lk, _ptr(bucket.contiguous()), _ptr(table.contiguous()), _ptr(out), _stream()),
+           "mmfd_rel_bias")
+    return out
+
+
+# ---- convolution support (ResNet50 extractor) ------------------------------------------------
+def conv_weight_prep(w, dtype, Kpad=None, bn=None, eps=1e-5):
+    """fp32 conv weight [Cout, Cin, KH, KW] (+ BatchNorm (gamma, beta, mean, var)) -> GEMM weight
+    [Cout, Kpad] in dtype with (kh, kw, c) column order, and the folded fp32 bias [Cout]."""
+    Cout, Cin, KH, KW = w.shape
+    Kpad = Kpad or KH * KW * Cin
+    ow = torch.empty((Cout, Kpad), device=w.device, dtype=dtype)
+    ob = torch.empty(Cout, device=w.device, dtype=torch.float32)
+    g, b, m, v = bn if bn is not None else (None, None, None, None)
+    _check(lib().mmfd_conv_weight_prep(dtype_code(dtype), Cout, Cin, KH, KW, Kpad, _ptr(w.contiguous()),
+                                       _ptr(g) if g is not None else None, _ptr(b) if b is not None else None,
+                                       _ptr(m) if m is not None else None, _ptr(v) if v is not None else None,
+                                       float(eps), _ptr(ow), _ptr(ob), _stream()), "mmfd_conv_weight_prep")
+    return ow, ob
+
+
+def im2col_nhwc(x, N, H, W, C, k, stride, pad, Kpad=None):
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    Kpad = Kpad or k * k * C
+    out = torch.empty((N * Ho * Wo, Kpad), device=x.device, dtype=x.dtype)
+    _check(lib().mmfd_im2col_nhwc(dtype_code(x.dtype), N, H, W, C, k, k, stride, pad, Ho, Wo, Kpad, _ptr(x), _ptr(out),
+                                  _stream()), "mmfd_im2col_nhwc")
+    return out, Ho, Wo
+
+
+def im2col_nchw(x, k, stride, pad, Kpad, dtype):
+    N, C, H, W = x.shape
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = torch.empty((N * Ho * Wo, Kpad), device=x.device, dtype=dtype)
+    _check(lib().mmfd_im2col_nchw(dtype_code(dtype), N, C, H, W, k, k, stride, pad, Ho, Wo, Kpad,
+                                  _ptr(x.contiguous()), _ptr(out), _stream()), "mmfd_im2col_nchw")
+    return out, Ho, Wo
+
+
+def maxpool_nhwc(x, N, H, W, C, k=3, stride=2, pad=1):
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = torch.empty((N * Ho * Wo, C), device=x.device, dtype=x.dtype)
+    _check(lib().mmfd_maxpool_nhwc(dtype_code(x.dtype), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(x), _ptr(out),
+                                   _stream()), "mmfd_maxpool_nhwc")
+    return out, Ho, Wo
+
+
+def global_avgpool(x, N, HW, C):
+    out = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    _check(lib().mmfd_global_avgpool(dtype_code(x.dtype), N, HW, C, _ptr(x), _ptr(out), _stream()),
+           "mmfd_global_avgpool")
+    return out
 
 
 def embed_bwd(ids, tts, dsum, dword, dpos, dtype_emb, padding_idx=-1):

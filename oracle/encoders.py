@@ -90,3 +90,54 @@ def vit_forward(P, pixel_values, *, num_layers, num_heads, patch=16, eps=1e-12, 
         h = F.layer_norm(x, (D,), P[p + ".layernorm_after.weight"], P[p + ".layernorm_after.bias"], eps)
         x = _lin(P, p + ".output.dense", F.gelu(_lin(P, p + ".intermediate.dense", h))) + x
     return F.layer_norm(x, (D,), P["layernorm.weight"], P["layernorm.bias"], eps)
+
+
+# ---- MPNet (bi-encoder of the text evidence corpus, text2text_retrieval.py:21,125,129-157) -------
+def mpnet_position_ids(input_ids, padding_idx=1):
+    """HF create_position_ids_from_input_ids"""
+    m = input_ids.ne(padding_idx).int()
+    return (torch.cumsum(m, dim=1).type_as(m) * m).long() + padding_idx
+
+
+def mpnet_buckets(L, num_buckets=32, max_distance=128):
+    """HF MPNetEncoder.relative_position_bucket over arange positions"""
+    import math
+    rel = torch.arange(L)[None, :] - torch.arange(L)[:, None]
+    n = -rel
+    nb = num_buckets // 2
+    ret = (n < 0).long() * nb
+    n = n.abs()
+    max_exact = nb // 2
+    large = max_exact + (torch.log(n.float() / max_exact) / math.log(max_distance / max_exact) * (nb - max_exact)).long()
+    large = torch.min(large, torch.full_like(large, nb - 1))
+    return ret + torch.where(n < max_exact, n, large)
+
+
+def mpnet_forward(P, input_ids, attention_mask=None, *, num_layers, num_heads, eps=1e-5, num_buckets=32,
+                  padding_idx=1):
+    """HF MPNetModel.last_hidden_state (eval): word + position (padding-aware ids) embeddings,
+    LayerNorm; post-LN layers whose attention adds the shared relative-position bias and the
+    extended mask; GELU FFN."""
+    B, L = input_ids.shape
+    pos = mpnet_position_ids(input_ids, padding_idx)
+    x = F.embedding(input_ids, P["embeddings.word_embeddings.weight"]) + \
+        F.embedding(pos, P["embeddings.position_embeddings.weight"])
+    D = x.shape[-1]
+    x = F.layer_norm(x, (D,), P["embeddings.LayerNorm.weight"], P["embeddings.LayerNorm.bias"], eps)
+    bias = F.embedding(mpnet_buckets(L, num_buckets), P["encoder.relative_attention_bias.weight"])  # [L, L, H]
+    bias = bias.permute(2, 0, 1)[None]
+    add = extended_mask(attention_mask)[:, None, None, :] if attention_mask is not None else 0.0
+    H, hd = num_heads, D // num_heads
+    for i in range(num_layers):
+        p = f"encoder.layer.{i}"
+        q = _lin(P, p + ".attention.attn.q", x).reshape(B, L, H, hd).transpose(1, 2)
+        k = _lin(P, p + ".attention.attn.k", x).reshape(B, L, H, hd).transpose(1, 2)
+        v = _lin(P, p + ".attention.attn.v", x).reshape(B, L, H, hd).transpose(1, 2)
+        s = torch.matmul(q, k.transpose(-1, -2)) / (hd ** 0.5) + bias + add
+        c = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, L, D)
+        x = F.layer_norm(_lin(P, p + ".attention.attn.o", c) + x, (D,), P[p + ".attention.LayerNorm.weight"],
+                         P[p + ".attention.LayerNorm.bias"], eps)
+        f = F.gelu(_lin(P, p + ".intermediate.dense", x))
+        x = F.layer_norm(_lin(P, p + ".output.dense", f) + x, (D,), P[p + ".output.LayerNorm.weight"],
+                         P[p + ".output.LayerNorm.bias"], eps)
+    return x

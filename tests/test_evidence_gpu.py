@@ -1,0 +1,185 @@
+"""Evidence-corpus extractors (SURVEY §8 a12 ResNet50, a13 MPNet) on the HIP path vs the
+transformers-generated fixtures and the CPU oracle.
+
+Tolerances: fp32 — max abs error 1e-4 relative to the output's max magnitude (1e-3 at full
+ResNet50 depth, where 53 folded-BN convolutions accumulate rounding); bf16 — 5e-2 relative
+(bf16 activations between layers, fp32 accumulation). Conv kernels (im2col, max/avg pool) are
+bit-exact data movement / fp32 reductions checked against torch.
+"""
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import mmfd
+from mmfd import kernels as K
+from mmfd.encoders import MPNetConfig, MPNetModel
+from mmfd.evidence import ImageCorpus, ImageSimilarity, ResNet, SentenceEncoder, preprocess, resnet50
+from oracle import encoders as OE
+from oracle.resnet import resnet_forward
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def _rel(got, ref):
+    got, ref = torch.as_tensor(got).double().cpu(), torch.as_tensor(ref).double().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+
+
+def _resnet_from_fixture(z, precision):
+    m = ResNet(tuple(z["depths"].tolist()), int(z["width"]))
+    sd = {k[len("param/"):]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("param/")}
+    m.load_state_dict(sd, strict=False)
+    return m.to(DEV).set_precision(precision)
+
+
+# ---- kernels --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,stride,pad", [(3, 1, 1), (3, 2, 1), (1, 2, 0), (7, 2, 3)])
+def test_im2col_nhwc_exact(dtype, k, stride, pad):
+    N, H, W, C = 2, 9, 11, 16
+    x = torch.randn(N, H, W, C).to(dtype)
+    cols, Ho, Wo = K.im2col_nhwc(x.to(DEV).view(N * H * W, C), N, H, W, C, k, stride, pad, Kpad=k * k * C + 8)
+    ref = F.unfold(x.permute(0, 3, 1, 2).float(), k, padding=pad, stride=stride)  # [N, C*k*k, L], (c, kh, kw)
+    ref = ref.view(N, C, k, k, -1).permute(0, 4, 2, 3, 1).reshape(N * Ho * Wo, k * k * C)
+    got = cols.float().cpu()
+    assert torch.equal(got[:, :k * k * C], ref.to(dtype).float())
+    assert torch.count_nonzero(got[:, k * k * C:]) == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_im2col_maxpool_avgpool(dtype):
+    x = torch.randn(2, 3, 20, 18)
+    cols, Ho, Wo = K.im2col_nchw(x.to(DEV), 7, 2, 3, 152, dtype)
+    ref = F.unfold(x, 7, padding=3, stride=2).view(2, 3, 7, 7, -1).permute(0, 4, 2, 3, 1).reshape(2 * Ho * Wo, 147)
+    assert torch.equal(cols.float().cpu()[:, :147], ref.to(dtype).float())
+    y = torch.randn(2, 10, 9, 32).to(dtype)
+    mp, Ho, Wo = K.maxpool_nhwc(y.to(DEV).view(-1, 32), 2, 10, 9, 32)
+    ref = F.max_pool2d(y.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).reshape(-1, 32)
+    assert torch.equal(mp.float().cpu(), ref)
+    ap = K.global_avgpool(y.to(DEV).view(-1, 32), 2, 90, 32)
+    assert (ap.cpu() - y.float().mean((1, 2))).abs().max().item() < 1e-5
+
+
+# ---- ResNet (a12) -----------------------------------------------------------------------------------
+def test_resnet_small_matches_fixture_fp32():
+    z = _load("resnet_small.npz")
+    m = _resnet_from_fixture(z, "fp32")
+    out = m(torch.from_numpy(z["pixel_values"]).to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(out, z["out"]) < 1e-4
+
+
+def test_resnet_small_bf16_close():
+    z = _load("resnet_small.npz")
+    m = _resnet_from_fixture(z, "bf16")
+    out = m(torch.from_numpy(z["pixel_values"]).to(DEV))
+    assert _rel(out, z["out"]) < 5e-2
+
+
+def test_resnet50_full_vs_oracle():
+    """full resnet50 at 224x224 (random init, non-trivial BN statistics) vs the CPU oracle"""
+    torch.manual_seed(0)
+    m = resnet50()
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
+                mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) + 0.5)
+                mod.weight.copy_(torch.rand(mod.weight.shape, generator=g) * 0.5 + 0.5)
+    P = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 3, 224, 224, generator=g)
+    ref = resnet_forward(P, x)
+    m = m.to(DEV)
+    out = m.set_precision("fp32")(x.to(DEV))
+    assert _rel(out, ref) < 1e-3
+    outb = m.set_precision("bf16")(x.to(DEV))
+    assert _rel(outb, ref) < 5e-2
+
+
+def test_image_similarity_and_corpus(tmp_path):
+    from PIL import Image
+    rng = np.random.default_rng(0)
+    for i in range(5):
+        Image.fromarray(rng.integers(0, 255, (40 + i, 50, 3), dtype=np.uint8)).save(tmp_path / f"img{i}.png")
+    (tmp_path / "notes.txt").write_text("skip me")
+    ext = ImageSimilarity(model=ResNet((1, 1, 1, 1), 8), precision="fp32")
+    f = ext.extract_features(str(tmp_path / "img0.png"))
+    assert f.shape == (256,) and f.device.type == "cpu"
+    buf = io.BytesIO()
+    Image.open(tmp_path / "img0.png").save(buf, format="PNG")
+    buf.seek(0)
+    assert torch.allclose(ext.extract_features(buf), f)
+    assert abs(ImageSimilarity.similarity(f, f) - 1.0) < 1e-9
+    corpus = ImageCorpus(str(tmp_path / "feats.npz"), extractor=ext, batch_size=2)
+    corpus.create_feature_corpus(str(tmp_path))
+    assert len(corpus.feature_dict) == 5
+    again = ImageCorpus(str(tmp_path / "feats.npz"), extractor=ext)
+    assert set(again.feature_dict) == set(corpus.feature_dict)
+    p0 = str(tmp_path / "img0.png")
+    assert torch.allclose(again.feature_dict[p0], f, atol=1e-5)
+    # batched and single extraction agree
+    batch = torch.stack([preprocess(str(tmp_path / f"img{i}.png")) for i in range(5)])
+    fb = ext.extract_batch(batch).cpu()
+    assert (fb[0] - f).abs().max().item() < 1e-4
+
+
+# ---- MPNet (a13) ------------------------------------------------------------------------------------
+def _mpnet_from_fixture(z, precision):
+    cfg = json.loads(str(z["config"]))
+    m = MPNetModel(MPNetConfig(vocab_size=cfg["vocab_size"], hidden_size=cfg["hidden_size"],
+                               num_hidden_layers=cfg["num_hidden_layers"], num_attention_heads=cfg["num_attention_heads"],
+                               intermediate_size=cfg["intermediate_size"],
+                               max_position_embeddings=cfg["max_position_embeddings"],
+                               layer_norm_eps=cfg["layer_norm_eps"]))
+    sd = {k[len("param/"):]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("param/")}
+    sd.pop("embeddings.position_ids", None)
+    m.load_state_dict(sd)
+    return m.to(DEV).set_precision(precision)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 5e-2)])
+def test_mpnet_small_matches_fixture(precision, tol):
+    z = _load("mpnet_small.npz")
+    m = _mpnet_from_fixture(z, precision)
+    out = m(input_ids=torch.from_numpy(z["input_ids"]), attention_mask=torch.from_numpy(z["attention_mask"]))
+    torch.cuda.synchronize()
+    assert _rel(out.last_hidden_state, z["out"]) < tol
+
+
+def test_sentence_encoder_cls_pooling_and_batching():
+    z = _load("mpnet_small.npz")
+    enc = SentenceEncoder(model=_mpnet_from_fixture(z, "fp32"), precision="fp32")
+    ids, mask = torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"])
+    e = enc.encode_ids(ids, mask, batch_size=2).cpu()
+    assert e.shape == (3, 64) and e.dtype == torch.float32
+    assert _rel(e, torch.from_numpy(z["out"])[:, 0]) < 1e-4
+    with pytest.raises(RuntimeError):
+        enc.encode(["no tokenizer here"])
+
+
+def test_mpnet_base_vs_oracle_l128():
+    """multi-qa-mpnet-base-dot-v1 architecture (random init) at the corpus length 128 vs oracle"""
+    torch.manual_seed(3)
+    m = MPNetModel(MPNetConfig())
+    P = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(3, 30527, (2, 128), generator=g)
+    mask = torch.ones_like(ids)
+    mask[1, 70:] = 0
+    ids[1, 70:] = 1
+    ref = OE.mpnet_forward(P, ids, mask, num_layers=12, num_heads=12)
+    out = m.to(DEV).set_precision("fp32")(input_ids=ids, attention_mask=mask).last_hidden_state
+    assert _rel(out, ref) < 1e-3

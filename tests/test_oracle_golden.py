@@ -132,3 +132,48 @@ def test_bert_vit_base_recipe():
     with torch.no_grad():
         out = OE.vit_forward(P, _t(z["pixel_values"]).float(), num_layers=12, num_heads=12)
     _close(out, z["out"], 5e-5)
+
+
+# ---- evidence extractors (a12 ResNet50, a13 MPNet) ----------------------------------------------
+def test_oracle_resnet_matches_transformers_fixture():
+    from oracle.resnet import resnet_forward
+    z = _load("resnet_small.npz")
+    out = resnet_forward(_params(z, "param/"), _t(z["pixel_values"]), depths=tuple(z["depths"].tolist()))
+    _close(out, z["out"])
+
+
+def test_oracle_mpnet_matches_transformers_fixture():
+    z = _load("mpnet_small.npz")
+    cfg = json.loads(str(z["config"]))
+    out = OE.mpnet_forward(_params(z, "param/"), _t(z["input_ids"]), _t(z["attention_mask"]),
+                           num_layers=cfg["num_hidden_layers"], num_heads=cfg["num_attention_heads"],
+                           eps=cfg["layer_norm_eps"])
+    _close(out, z["out"])
+
+
+def test_mpnet_buckets_product_host_code_matches_oracle():
+    """the product computes the bucket map on the host once per length; it must equal HF's"""
+    from mmfd.encoders import mpnet_relative_buckets
+    for L in (1, 7, 40, 128, 300, 512):
+        assert torch.equal(mpnet_relative_buckets(L).long(), OE.mpnet_buckets(L))
+
+
+def test_extractor_state_dict_names():
+    from mmfd.encoders import MPNetConfig, MPNetModel
+    from mmfd.evidence import ResNet, resnet50
+    z = _load("resnet_small.npz")
+    mine = {k: tuple(v.shape) for k, v in ResNet((1, 1, 2, 1), 8).state_dict().items()
+            if "num_batches" not in k and not k.startswith("fc.")}
+    ref = {k[len("param/"):]: tuple(z[k].shape) for k in z.files if k.startswith("param/")}
+    assert mine == ref
+    assert sum(p.numel() for p in resnet50().parameters()) == 25_557_032  # torchvision resnet50
+    zm = _load("mpnet_small.npz")
+    cfg = json.loads(str(zm["config"]))
+    m = MPNetModel(MPNetConfig(vocab_size=cfg["vocab_size"], hidden_size=cfg["hidden_size"],
+                               num_hidden_layers=cfg["num_hidden_layers"], num_attention_heads=cfg["num_attention_heads"],
+                               intermediate_size=cfg["intermediate_size"],
+                               max_position_embeddings=cfg["max_position_embeddings"]))
+    mine = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    ref = {k[len("param/"):]: tuple(zm[k].shape) for k in zm.files if k.startswith("param/")}
+    ref.pop("embeddings.position_ids", None)
+    assert mine == ref
