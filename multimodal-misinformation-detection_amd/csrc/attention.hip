@@ -178,6 +178,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
   uint4 qf[C::KCH];
   load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
 
   float m = -INFINITY, lsum = 0.f;
   f32x4 o[C::DT];
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
         float pe = e;
         if (p.p > 0.f) {
           const int64_t key = k0 + ks * 16 + 4 * g + r;
-          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
           pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
         }
         s[ks][r] = pe;
@@ -310,6 +311,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
   const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
 
   uint4 kf[C::KCH], vf[C::KCH];
   load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
@@ -353,7 +355,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
         }
         float z = 1.f;
         if (p.p > 0.f) {
-          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + q) * p.Lk + mykey));
+          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + q) * p.Lk + mykey));
           z = (hsh < p.thr) ? 0.f : p.keep_scale;
         }
         pd[qs][r] = pr * z;
@@ -411,6 +413,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
   const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
 
   uint4 qf[C::KCH], dof[C::KCH];
   load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
@@ -449,7 +452,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
         }
         float z = 1.f;
         if (p.p > 0.f) {
-          const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
           z = (hsh < p.thr) ? 0.f : p.keep_scale;
         }
         ds[ks][r] = pr * (dp[r] * z - dlt);
@@ -522,6 +525,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   stage_all<T, D, true>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
   __syncthreads();
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
@@ -568,7 +572,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
           rs += e;
           float pe = e;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash(seed, p.salt, hbase + (uint64_t)(k0 + ks * 16 + 4 * g + r));
+            const uint32_t hsh = mmfd_hash_k(hkey, hbase + (uint64_t)(k0 + ks * 16 + 4 * g + r));
             pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
           }
           s[ks][r] = pe;
@@ -638,6 +642,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * p.D;
   T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const int nkb = (int)((p.Lk + 15) / 16);
   const int nqc = lq_pad / 32;  // 32-query chunks
   for (int kbk = wave; kbk < nkb; kbk += V2_DKDV_THREADS / 64) {
@@ -670,7 +675,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
           }
           float z = 1.f;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + lq) * p.Lk + mykey));
+            const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + lq) * p.Lk + mykey));
             z = (hsh < p.thr) ? 0.f : p.keep_scale;
           }
           pd[h2][r] = pr * z;
@@ -727,6 +732,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const int nqb = (int)((p.Lq + 15) / 16);
   const int nkc = lk_pad / 32;
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
@@ -761,7 +767,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
           }
           float z = 1.f;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash(seed, p.salt, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+            const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
             z = (hsh < p.thr) ? 0.f : p.keep_scale;
           }
           ds[h2][r] = pr * (dp[r] * z - dlt);

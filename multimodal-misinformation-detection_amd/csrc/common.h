@@ -63,13 +63,18 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 __host__ __device__ __forceinline__ uint32_t mmfd_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
 }
+// per-call key from (seed, salt): loop invariant, hoisted out of every element loop
+__host__ __device__ __forceinline__ uint32_t mmfd_hash_key(uint64_t seed, uint64_t salt) {
+  const uint32_t k0 = mmfd_mix32((uint32_t)seed ^ mmfd_mix32((uint32_t)(seed >> 32) ^ 0x85ebca6bu));
+  return mmfd_mix32(k0 ^ (uint32_t)salt ^ mmfd_mix32((uint32_t)(salt >> 32) ^ 0xc2b2ae35u));
+}
+// one mix round per element: the index enters through odd multipliers (a bijection of the low
+// word for a fixed high word)
+__host__ __device__ __forceinline__ uint32_t mmfd_hash_k(uint32_t key, uint64_t idx) {
+  return mmfd_mix32(key ^ ((uint32_t)idx * 0x9e3779b1u) ^ ((uint32_t)(idx >> 32) * 0x85ebca77u));
+}
 __host__ __device__ __forceinline__ uint32_t mmfd_hash(uint64_t seed, uint64_t salt, uint64_t idx) {
-  uint32_t h = mmfd_mix32((uint32_t)idx);
-  h = mmfd_mix32(h ^ (uint32_t)(idx >> 32) ^ 0x9e3779b9u);
-  h = mmfd_mix32(h ^ (uint32_t)salt ^ ((uint32_t)(salt >> 32) * 0x85ebca6bu));
-  h = mmfd_mix32(h ^ (uint32_t)seed);
-  h = mmfd_mix32(h ^ (uint32_t)(seed >> 32));
-  return h;
+  return mmfd_hash_k(mmfd_hash_key(seed, salt), idx);
 }
 // threshold so that keep <=> hash >= thr, i.e. P(drop) = p
 __host__ __device__ __forceinline__ uint32_t mmfd_drop_threshold(float p) {

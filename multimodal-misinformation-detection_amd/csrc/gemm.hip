@@ -44,7 +44,7 @@ struct EpiArgs {
 
 template <typename TC>
 __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t ldc, int64_t N,
-                                               int64_t row, int64_t col, float z, uint64_t seed) {
+                                               int64_t row, int64_t col, float z, uint32_t hkey) {
   if (e.bias) z += e.bias[col];
   if (e.res_first && e.residual) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
   if (e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU) {
@@ -56,7 +56,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
     z = (to_f32(reinterpret_cast<const TC*>(e.aux)[row * e.ldaux + col]) > 0.0f) ? z : 0.0f;
   }
   if (e.p > 0.0f) {
-    const uint32_t h = mmfd_hash(seed, e.salt, (uint64_t)row * (uint64_t)N + (uint64_t)col);
+    const uint32_t h = mmfd_hash_k(hkey, (uint64_t)row * (uint64_t)N + (uint64_t)col);
     z = (h < e.thr) ? 0.0f : z * e.keep_scale;
   }
   if (e.residual && !e.res_first) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
@@ -92,7 +92,7 @@ template <> struct V8<float> {
 // 8 consecutive columns [col, col+8) of one row; same operation order as epilogue_store
 template <typename TC>
 __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t ldc, int64_t N, int64_t row,
-                                                int64_t col, float (&z)[8], uint64_t seed) {
+                                                int64_t col, float (&z)[8], uint32_t hkey) {
   if (e.bias) {
     const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col), b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
     z[0] += b0.x; z[1] += b0.y; z[2] += b0.z; z[3] += b0.w; z[4] += b1.x; z[5] += b1.y; z[6] += b1.z; z[7] += b1.w;
@@ -126,7 +126,7 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
   if (e.p > 0.0f) {
     const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)col;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) z[q] = (mmfd_hash(seed, e.salt, base + q) < e.thr) ? 0.0f : z[q] * e.keep_scale;
+    for (int q = 0; q < 8; ++q) z[q] = (mmfd_hash_k(hkey, base + q) < e.thr) ? 0.0f : z[q] * e.keep_scale;
   }
   if (e.residual && !e.res_first) {
     float r[8];
@@ -326,7 +326,7 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
   constexpr int LDC = BN + 4;
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
-  const uint64_t seed = (!ws && e.p > 0.0f) ? *e.seed : 0ull;
+  const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
   for (int qtr = 0; qtr < 4; ++qtr) {
@@ -561,7 +561,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   constexpr int LDC = G8_BN + 4;
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
-  const uint64_t seed = (!ws && e.p > 0.0f) ? *e.seed : 0ull;
+  const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -611,7 +611,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
                                      int64_t ldc, int64_t M, int64_t N, EpiArgs e) {
-  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+  const uint32_t seed = (e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   const int64_t total = M * N;
   if (e.vec && (N % 8) == 0) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total / 8; g += (int64_t)gridDim.x * blockDim.x) {
@@ -638,7 +638,7 @@ template <typename T, typename TC>
 __global__ void gemm_simple_kernel(const T* __restrict__ A, int64_t lda, int ta, const T* __restrict__ B,
                                    int64_t ldb, int tb, TC* __restrict__ C, int64_t ldc, int64_t M,
                                    int64_t N, int64_t K, float alpha, EpiArgs e) {
-  const uint64_t seed = (e.p > 0.0f) ? *e.seed : 0ull;
+  const uint32_t seed = (e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   const int64_t total = M * N;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {

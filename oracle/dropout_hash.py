@@ -23,20 +23,21 @@ def mix32(x):
     return x
 
 
+def _key(seed: int, salt: int):
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    k0 = mix32(np.uint32(seed & 0xFFFFFFFF) ^ mix32(np.uint32(seed >> 32) ^ np.uint32(0x85EBCA6B)))
+    return mix32(k0 ^ np.uint32(salt & 0xFFFFFFFF) ^ mix32(np.uint32(salt >> 32) ^ np.uint32(0xC2B2AE35)))
+
+
 def dropout_hash(seed: int, salt: int, idx):
+    """mmfd_hash(seed, salt, idx) = mix32(key ^ lo*0x9E3779B1 ^ hi*0x85EBCA77), key = mmfd_hash_key"""
     idx = np.asarray(idx, dtype=np.uint64)
     lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     hi = (idx >> np.uint64(32)).astype(np.uint32)
-    salt = int(salt) & 0xFFFFFFFFFFFFFFFF
-    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     with np.errstate(over="ignore"):
-        h = mix32(lo)
-        h = mix32(h ^ hi ^ np.uint32(0x9E3779B9))
-        s_hi = np.uint32(((salt >> 32) * 0x85EBCA6B) & 0xFFFFFFFF)
-        h = mix32(h ^ np.uint32(salt & 0xFFFFFFFF) ^ s_hi)
-        h = mix32(h ^ np.uint32(seed & 0xFFFFFFFF))
-        h = mix32(h ^ np.uint32(seed >> 32))
-    return h
+        x = (lo * np.uint32(0x9E3779B1)).astype(np.uint32) ^ (hi * np.uint32(0x85EBCA77)).astype(np.uint32)
+        return mix32(_key(seed, salt) ^ x)
 
 
 def drop_threshold(p: float) -> int:

@@ -79,3 +79,19 @@ def test_forward_on_cpu_fails_loudly():
     m = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, hidden_dim=16)
     with pytest.raises(RuntimeError):
         m(torch.randn(1, 3, 48), torch.randn(1, 3, 40), torch.randn(1, 3, 48), torch.randn(1, 3, 40))
+
+
+def test_dropout_hash_statistics():
+    """the one-round counter hash: keep rate within 3 sigma of 1-p over 2^20 consecutive indices,
+    no correlation between neighbouring elements, different salts give independent masks"""
+    from oracle.dropout_hash import keep_mask
+    n = 1 << 20
+    for p in (0.1, 0.5):
+        k = keep_mask(1234, salt_of("stats"), (n,), p).astype(np.float64)
+        sigma = (p * (1 - p) / n) ** 0.5
+        assert abs(k.mean() - (1 - p)) < 3 * sigma
+        c = np.corrcoef(k[:-1], k[1:])[0, 1]
+        assert abs(c) < 5 / n ** 0.5
+    a = keep_mask(7, salt_of("a"), (n,), 0.5).astype(np.float64)
+    b = keep_mask(7, salt_of("b"), (n,), 0.5).astype(np.float64)
+    assert abs(np.corrcoef(a, b)[0, 1]) < 5 / n ** 0.5
