@@ -25,6 +25,8 @@ class StepCtx:
         self._w = {}             # cached compute-dtype weights
         self.grads = {}          # name -> fp32 grad tensor
         self._written = set()
+        self.grad_ready = None   # optional callable(names, grads): finished gradients (DP overlap)
+        self._notified = set()
 
     # ---- weights -------------------------------------------------------------------------------
     def w(self, name):
@@ -70,6 +72,15 @@ class StepCtx:
         return dict(dropout_p=self.p, seed=self.seed, salt=K.salt_of(site))
 
     # ---- gradients -----------------------------------------------------------------------------
+    def flush_ready(self):
+        """report the gradients written since the last call as final (a layer's backward is done)"""
+        if self.grad_ready is None:
+            return
+        names = [n for n in self.grads if n not in self._notified]
+        if names:
+            self._notified.update(names)
+            self.grad_ready(names, self.grads)
+
     def grad_slot(self, pname, shape):
         """(tensor, beta) for accumulating into the gradient of parameter `pname`."""
         g = self.grads.get(pname)

@@ -2,8 +2,11 @@
 
 The reference is single-device (train.py:321); the batch dimension shards naturally (independent
 claim/evidence pairs), so each rank runs the full step on its own 256 pairs and the only exchange is
-the gradient all-reduce. Gradients are packed into ~64 MB fp32 buckets (few, large collectives suit
-the point-to-point xGMI rings), all-reduced with op AVG, and unpacked.
+the gradient average. The all-reduce is OVERLAPPED with the backward pass: the hand-written
+backward of each encoder reports every layer's finished parameter gradients (StepCtx.flush_ready),
+they are packed into ~32 MB fp32 buckets and each full bucket is all-reduced asynchronously on
+RCCL's stream while the next layers' backward kernels run on the compute stream. `finish()` waits
+for the outstanding buckets and writes the averages into the parameters' .grad.
 """
 from __future__ import annotations
 
@@ -26,41 +29,76 @@ class GradAllReduce:
     kernels; they are parameters only so the bucketing + collective logic can be exercised on the
     CPU (gloo) in tests."""
 
-    def __init__(self, bucket_mb: float = 64.0, group=None, pack=_pack, unpack=_unpack):
+    def __init__(self, bucket_mb: float = 32.0, group=None, pack=_pack, unpack=_unpack):
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
         self.group = group
         self._bufs = {}
         self._pack, self._unpack = pack, unpack
+        self.begin()
 
-    def _buckets(self, grads):
-        bucket, n = [], 0
-        for g in grads:
-            if bucket and n + g.numel() > self.bucket_elems:
-                yield bucket, n
-                bucket, n = [], 0
-            bucket.append(g)
-            n += g.numel()
-        if bucket:
-            yield bucket, n
+    # ---- per-step protocol ------------------------------------------------------------------------
+    def begin(self):
+        self._pending, self._pending_n = [], 0
+        self._works = []
+        self._nbucket = 0
 
-    def allreduce_grads(self, params):
-        grads = [p.grad for p in params if p.grad is not None]
-        if not grads or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+    def ready(self, pairs):
+        """pairs: iterable of (parameter, finished fp32 gradient tensor)"""
+        if not self._active():
             return
+        for p, g in pairs:
+            if g is None:
+                continue
+            self._pending.append((p, g))
+            self._pending_n += g.numel()
+            if self._pending_n >= self.bucket_elems:
+                self._flush()
+
+    def hook_for(self, model):
+        """callable(names, grads) for StepCtx.grad_ready: maps parameter names of `model` to params"""
+        params = dict(model.named_parameters())
+        return lambda names, grads: self.ready((params[n], grads[n]) for n in names if n in params)
+
+    def finish(self):
+        """flush, wait, and write the averages into each parameter's .grad (the tensor autograd
+        installed, which may or may not be the one that was packed)"""
+        if not self._active():
+            return
+        self._flush()
         world = dist.get_world_size(self.group)
-        works = []
-        for i, (bucket, n) in enumerate(self._buckets(grads)):
-            buf = self._bufs.get(i)
-            if buf is None or buf.numel() < n or buf.device != bucket[0].device:
-                buf = self._bufs[i] = torch.empty(n, device=bucket[0].device, dtype=torch.float32)
-            off = 0
-            for g in bucket:
-                self._pack(g, buf[off:off + g.numel()])
-                off += g.numel()
-            works.append((dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True), bucket, buf))
-        for w, bucket, buf in works:
+        for w, items, buf in self._works:
             w.wait()
             off = 0
-            for g in bucket:
-                self._unpack(buf[off:off + g.numel()], g, 1.0 / world)
-                off += g.numel()
+            for p, g in items:
+                n = g.numel()
+                self._unpack(buf[off:off + n], p.grad if p.grad is not None else g, 1.0 / world)
+                off += n
+        self.begin()
+
+    def allreduce_grads(self, params):
+        """non-overlapped form: average every .grad of `params`"""
+        self.begin()
+        self.ready((p, p.grad) for p in params)
+        self.finish()
+
+    # ---- internals -----------------------------------------------------------------------------------
+    def _active(self):
+        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def _flush(self):
+        if not self._pending:
+            return
+        items, n = self._pending, self._pending_n
+        self._pending, self._pending_n = [], 0
+        i = self._nbucket
+        self._nbucket += 1
+        dev = items[0][1].device
+        buf = self._bufs.get(i)
+        if buf is None or buf.numel() < n or buf.device != dev:
+            buf = self._bufs[i] = torch.empty(max(n, self.bucket_elems), device=dev, dtype=torch.float32)
+        off = 0
+        for _, g in items:
+            self._pack(g, buf[off:off + g.numel()])
+            off += g.numel()
+        work = dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._works.append((work, items, buf))

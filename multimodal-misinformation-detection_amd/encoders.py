@@ -190,6 +190,7 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         Wp, _ = ctx.w_packed(names)
         Bk.linear_dx(ctx, dq2, Wp, out=ds1, beta=1.0)  # dx_in
         dx = ds1
+        ctx.flush_ready()
     # embeddings: undo the embedding dropout, LayerNorm backward, scatter into the tables
     if st["emb_drop"]:
         dx = K.dropout(dx, st["emb_drop"]["dropout_p"], st["emb_drop"]["seed"], st["emb_drop"]["salt"])
@@ -202,6 +203,7 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
     ctx.grads["embeddings.word_embeddings.weight"] = dword
     ctx.grads["embeddings.position_embeddings.weight"] = dpos
     ctx.grads["embeddings.token_type_embeddings.weight"] = dtyp
+    ctx.flush_ready()
 
 
 class _BertFn(torch.autograd.Function):
@@ -216,6 +218,7 @@ class _BertFn(torch.autograd.Function):
         dev = params[0].device
         sc = Bk.StepCtx(P, model.compute_dtype, p, model._fork_seed(dev) if training and p > 0 else None,
                         training=training)
+        sc.grad_ready = getattr(model, "_grad_ready", None)
         ids = input_ids.to(dev).long().contiguous()
         B, L = ids.shape
         mask = attention_mask.to(dev).long().contiguous() if attention_mask is not None else None
@@ -356,10 +359,12 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
         Wp, _ = ctx.w_packed(names)
         dh = Bk.linear_dx(ctx, dq2, Wp)
         dx, _ = Bk.layernorm_bwd(ctx, dh, x, p + ".layernorm_before", mb, rb, dx_add=dx1)
+        ctx.flush_ready()
     dpatch, dcls, dpos = K.vit_tokens_bwd(dx.view(st["B"], st["T"], D))
     ctx.grads["embeddings.cls_token"] = dcls.view(1, 1, D)
     ctx.grads["embeddings.position_embeddings"] = dpos.view(1, st["T"], D)
     ctx.lin_grads(["embeddings.patch_embeddings.projection"], dpatch, st["patches"])
+    ctx.flush_ready()
 
 
 class _ViTFn(torch.autograd.Function):
@@ -369,6 +374,7 @@ class _ViTFn(torch.autograd.Function):
         P[PATCH_W] = P[PATCH_W].reshape(P[PATCH_W].shape[0], -1)  # conv16/s16 == GEMM over patches
         dev = params[0].device
         sc = Bk.StepCtx(P, model.compute_dtype, 0.0, None, training=model.training)
+        sc.grad_ready = getattr(model, "_grad_ready", None)
         out, st = vit_forward(sc, model.config, pixel_values.to(dev).float().contiguous(), keep)
         fctx.keep = keep
         if keep:

@@ -115,6 +115,7 @@ class _HeadFn(torch.autograd.Function):
         P = {n: p.detach() for n, p in zip(names, params)}
         sc = Bk.StepCtx(P, model.compute_dtype, model.dropout_p, model._get_seed() if model.training else None,
                         training=model.training)
+        sc.grad_ready = getattr(model, "_grad_ready", None)
         outs, state = FU.head_forward(sc, model._cfg, X_t, X_i, E_t, E_i)
         ctx.sc, ctx.state, ctx.model = sc, state, model
         ctx.in_shapes = [None if x is None else (x.shape, x.dtype) for x in (X_t, X_i, E_t, E_i)]
@@ -138,6 +139,7 @@ class _HeadFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         dXt, dXi, dEt, dEi = FU.head_backward(sc, model._cfg, douts, state, need_dX=(need[1], need[2]),
                                               need_dE=(need[3], need[4]))
+        sc.flush_ready()
 
         def back(d, shp):
             if d is None or shp is None:

@@ -70,6 +70,9 @@ class FusionTrainer:
         self.params = params
         self.optimizer = AdamW(params, lr=lr)
         self.dp = dp
+        if dp is not None:  # overlap the gradient all-reduce with the backward pass
+            for m in ((head,) if freeze_encoders else (text_encoder, image_encoder, head)):
+                m._grad_ready = dp.hook_for(m)
 
     def step(self, batch):
         self.optimizer.zero_grad(set_to_none=True)
@@ -79,9 +82,11 @@ class FusionTrainer:
             I = self.image_encoder(batch["pixel_values"]).last_hidden_state
         outs = self.head(T[:B], I[:B], T[B:], I[B:])
         loss = path_losses(outs, batch["labels"])
+        if self.dp is not None:
+            self.dp.begin()
         loss[0].backward()
         if self.dp is not None:
-            self.dp.allreduce_grads(self.params)
+            self.dp.finish()
         self.optimizer.step()
         return loss
 

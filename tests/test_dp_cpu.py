@@ -41,7 +41,22 @@ def _worker(rank, world, port, bucket_mb, q):
             params.append(p)
         params.append(torch.zeros(3, requires_grad=True))  # no grad: skipped
         GradAllReduce(bucket_mb=bucket_mb, pack=_pack, unpack=_unpack).allreduce_grads(params)
-        q.put((rank, [p.grad.clone() if p.grad is not None else None for p in params]))
+        res = [p.grad.clone() if p.grad is not None else None for p in params]
+        # overlapped protocol: layers report finished gradients in backward order (hook_for maps
+        # names to parameters); the averages land in .grad at finish()
+        m = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Linear(7, 300))
+        grads = {}
+        for i, (n, p) in enumerate(m.named_parameters()):
+            grads[n] = torch.randn(p.shape, generator=torch.Generator().manual_seed(100 * rank + i))
+            p.grad = grads[n].clone()
+        dp = GradAllReduce(bucket_mb=bucket_mb, pack=_pack, unpack=_unpack)
+        hook = dp.hook_for(m)
+        dp.begin()
+        hook(["1.weight", "1.bias"], grads)
+        hook(["0.weight", "0.bias"], grads)
+        dp.finish()
+        res += [p.grad.clone() for p in m.parameters()]
+        q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
@@ -63,4 +78,9 @@ def test_grad_allreduce_gloo_world2(bucket_mb):
         want = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * r + i)) for r in range(world)) / world
         for r in range(world):
             torch.testing.assert_close(res[r][i], want, rtol=1e-6, atol=1e-6)
-    assert res[0][-1] is None and res[1][-1] is None
+    assert res[0][5] is None and res[1][5] is None
+    m = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Linear(7, 300))
+    for i, (n, p) in enumerate(m.named_parameters()):
+        want = sum(torch.randn(p.shape, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
+        for r in range(world):
+            torch.testing.assert_close(res[r][6 + i], want, rtol=1e-6, atol=1e-6)

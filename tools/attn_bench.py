@@ -1,0 +1,60 @@
+"""Attention kernels at the encoder shapes (bs=256 pairs -> 512 sequences x 12 heads, D=64):
+BERT L=128 with key mask + dropout 0.1, ViT L=197 without. Prints per-kernel-call times.
+python tools/attn_bench.py [--iters N] [--only bert|vit]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import mmfd  # noqa: E402
+from mmfd import kernels as K  # noqa: E402
+
+
+def case(name, L, masked, p, iters):
+    B, H, D = 512, 12, 64
+    dev = "cuda"
+    g = torch.Generator(device="cpu").manual_seed(0)
+    qkv = torch.randn(B, L, 3 * H * D, generator=g).to(dev, torch.bfloat16)
+    q, k, v = qkv[..., :H * D], qkv[..., H * D:2 * H * D], qkv[..., 2 * H * D:]
+    dout = torch.randn(B, L, H * D, generator=g).to(dev, torch.bfloat16)
+    kb = None
+    if masked:
+        mask = torch.ones(B, L, dtype=torch.long)
+        mask[::2, L * 3 // 4:] = 0
+        kb = K.mask_to_bias(mask.to(dev))
+    seed = K.Seed(5)
+    kw = dict(key_bias=kb, dropout_p=p, seed=seed, salt=K.salt_of("bench")) if p > 0 else dict(key_bias=kb)
+    o, lse = K.attn_fwd(q, k, v, H, **kw)
+    dq = torch.empty_like(q); dk = torch.empty_like(k); dv = torch.empty_like(v)
+    for _ in range(2):
+        K.attn_fwd(q, k, v, H, out=o, **kw)
+        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(iters):
+        ev[0].record()
+        K.attn_fwd(q, k, v, H, out=o, **kw)
+        ev[1].record()
+        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw)
+        ev[2].record()
+        torch.cuda.synchronize()
+        tf += ev[0].elapsed_time(ev[1])
+        tb += ev[1].elapsed_time(ev[2])
+    tf, tb = tf / iters, tb / iters
+    fl = 4.0 * B * H * L * L * D
+    print(f"{name}: fwd {tf * 1e3:7.1f} us ({fl / tf / 1e9:6.1f} TF/s)  bwd {tb * 1e3:7.1f} us "
+          f"({2.5 * fl / tb / 1e9:6.1f} TF/s)", flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    if a.only in ("", "bert"):
+        case("bert L=128 mask+drop", 128, True, 0.1, a.iters)
+    if a.only in ("", "vit"):
+        case("vit  L=197          ", 197, False, 0.0, a.iters)
