@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 // (all 16 S^T subtiles stay in registers, so no online rescaling).
 // =================================================================================================
 constexpr int V2_LMAX = 256;
-constexpr int V2_THREADS = 256;       // forward / dQ: 4 waves, several workgroups per CU
+constexpr int V2_THREADS = 512;       // forward / dQ: 8 waves sharing one K/V image
 constexpr int V2_DKDV_THREADS = 256;
 template <int D> struct V2 { static constexpr bool DUAL = (D == 64); };  // row image == transposed image
 
@@ -507,10 +507,20 @@ __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base,
   }
 }
 
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+
+// per-key additive bias in log2 units for the head's batch row: log2e * key_bias (clamped so a
+// fully masked row stays finite, as HF's finfo.min mask does) for k < Lk, -inf for padded keys
+template <int NTH>
+__device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t b, int npad, int tid) {
+  for (int i = tid; i < npad; i += NTH)
+    dst[i] = i < p.Lk ? (p.key_bias ? fmaxf(p.key_bias[b * p.Lk + i] * LOG2E, -1e30f) : 0.f) : -INFINITY;
+}
+
 template <int D>
 __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
-  // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax over
-  // 64-key chunks (few live registers -> several workgroups per CU overlap staging and compute)
+  // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
+  // domain) over 64-key chunks; key mask/padding come from a per-key bias vector in LDS
   using T = bf16;
   using C = AT<T, D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -520,19 +530,23 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   const int lk_pad = (int)((p.Lk + 63) & ~63);
   char* k_img = smem;
   char* v_img = smem + lk_pad * C::RB;
+  float* kbias = reinterpret_cast<float*>(smem + 2 * lk_pad * C::RB);
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   stage_all<T, D, false>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, tid, p.D);
   stage_all<T, D, true>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk_pad, tid);
   __syncthreads();
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH];
     load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
-    const uint64_t hbase = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
+    const float* relrow = p.rel_bias ? p.rel_bias + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[C::DT];
 #pragma unroll
@@ -549,30 +563,34 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4 kb4 = *reinterpret_cast<const float4*>(kbias + k0 + ks * 16 + 4 * g);
+        const float kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = k0 + ks * 16 + 4 * g + r;
-          float v = s[ks][r] * p.scale;
-          if (key >= p.Lk) v = -INFINITY;
-          else if (p.key_bias || p.rel_bias) v += bias_at(p, b, h, myq < p.Lq ? myq : 0, key);
-          s[ks][r] = v;
-          mx = fmaxf(mx, v);
+          float t = fmaf(s[ks][r], c2, kb[r]);
+          if (relrow) {
+            const int key = k0 + ks * 16 + 4 * g + r;
+            if (key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
+          }
+          s[ks][r] = t;
+          mx = fmaxf(mx, t);
         }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
-      const float alpha = __expf(m - mnew);
+      const float alpha = exp2f(m - mnew);
       float rs = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(s[ks][r] - mnew);
+          const float e = exp2f(s[ks][r] - mnew);
           rs += e;
           float pe = e;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, hbase + (uint64_t)(k0 + ks * 16 + 4 * g + r));
+            const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)(k0 + ks * 16 + 4 * g + r));
             pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
           }
           s[ks][r] = pe;
@@ -605,12 +623,13 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
           if (d * 16 + li < p.D) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
       }
     }
-    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = m + __logf(lsum);
+    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = (m + log2f(lsum)) * LN2;
   }
 }
 
 template <int D>
 __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) {
+  // Q/dO of the head resident in LDS (plus lse, delta in log2 units); each wave owns 16 keys
   using T = bf16;
   using C = AT<T, D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -626,6 +645,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   char* do_tr = DUAL ? do_row : smem + 3 * img;
   float* s_lse = reinterpret_cast<float*>(smem + (DUAL ? 2 : 4) * img);
   float* s_delta = s_lse + V2_LMAX;
+  float* kbias = s_delta + V2_LMAX;
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   stage_all<T, D, false, V2_DKDV_THREADS>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
@@ -633,9 +653,10 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   stage_all<T, D, false, V2_DKDV_THREADS>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
   if (!DUAL) stage_all<T, D, true, V2_DKDV_THREADS>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
   for (int i = tid; i < lq_pad; i += V2_DKDV_THREADS) {
-    s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] : INFINITY;
+    s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] * LOG2E : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
   }
+  stage_kbias<V2_DKDV_THREADS>(kbias, p, b, (int)((p.Lk + 15) & ~15), tid);
   __syncthreads();
   const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
   const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
@@ -643,6 +664,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
   const int nkb = (int)((p.Lk + 15) / 16);
   const int nqc = lq_pad / 32;  // 32-query chunks
   for (int kbk = wave; kbk < nkb; kbk += V2_DKDV_THREADS / 64) {
@@ -650,6 +672,8 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
     uint4 kf[C::KCH], vf[C::KCH];
     load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
     load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
+    const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
     f32x4 dk[C::DT], dv[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
@@ -664,22 +688,22 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
           Mma<T>::run(sv, row_frag<T, D>(q_row, qs, kc, lane), kf[kc]);
           Mma<T>::run(dp, row_frag<T, D>(do_row, qs, kc, lane), vf[kc]);
         }
+        const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qs * 16 + 4 * g);
+        const float4 d4 = *reinterpret_cast<const float4*>(s_delta + qs * 16 + 4 * g);
+        const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int lq = qs * 16 + 4 * g + r;
-          float pr = 0.f;
-          if (mykey < p.Lk) {
-            float sc = sv[r] * p.scale;
-            if ((p.key_bias || p.rel_bias) && lq < p.Lq) sc += bias_at(p, b, h, lq, mykey);
-            pr = __expf(sc - s_lse[lq]);
-          }
+          float t = fmaf(sv[r], c2, kb2);
+          if (p.rel_bias && lq < p.Lq && mykey < p.Lk) t = fmaf(p.rel_bias[(h * p.Lq + lq) * p.Lk + mykey], LOG2E, t);
+          const float pr = exp2f(t - lq2[r]);
           float z = 1.f;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + lq) * p.Lk + mykey));
+            const uint32_t hsh = mmfd_hash_k(hkey, hcol + (uint64_t)lq * (uint64_t)p.Lk);
             z = (hsh < p.thr) ? 0.f : p.keep_scale;
           }
           pd[h2][r] = pr * z;
-          ds[h2][r] = pr * (dp[r] * z - s_delta[lq]);
+          ds[h2][r] = pr * (dp[r] * z - dl[r]);
         }
       }
       const uint4 ap = pack_acc<T>(pd, 0);
@@ -711,6 +735,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
 
 template <int D>
 __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
+  // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K
   using T = bf16;
   using C = AT<T, D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -723,16 +748,19 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
   char* k_row = smem;
   char* v_row = smem + img;
   char* k_tr = DUAL ? k_row : smem + 2 * img;
+  float* kbias = reinterpret_cast<float*>(smem + (DUAL ? 2 : 3) * img);
   const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
   stage_all<T, D, false>(k_row, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
   if (!DUAL) stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
   stage_all<T, D, false>(v_row, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk_pad, tid);
   __syncthreads();
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
   const int nkc = lk_pad / 32;
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
@@ -740,8 +768,10 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
     uint4 qf[C::KCH], dof[C::KCH];
     load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
     load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
-    const float lse = myq < p.Lq ? p.lse[bh * p.Lq + myq] : INFINITY;
+    const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
     const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    const float* relrow = p.rel_bias ? p.rel_bias + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -756,18 +786,17 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
           Mma<T>::run(sv, row_frag<T, D>(k_row, ks, kc, lane), qf[kc]);
           Mma<T>::run(dp, row_frag<T, D>(v_row, ks, kc, lane), dof[kc]);
         }
+        const float4 kb4 = *reinterpret_cast<const float4*>(kbias + ks * 16 + 4 * g);
+        const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t key = ks * 16 + 4 * g + r;
-          float pr = 0.f;
-          if (key < p.Lk) {
-            float sc = sv[r] * p.scale;
-            if ((p.key_bias || p.rel_bias) && myq < p.Lq) sc += bias_at(p, b, h, myq, key);
-            pr = __expf(sc - lse);
-          }
+          const int key = ks * 16 + 4 * g + r;
+          float t = fmaf(sv[r], c2, kbr[r]);
+          if (relrow && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
+          const float pr = exp2f(t - lse2);
           float z = 1.f;
           if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
+            const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)key);
             z = (hsh < p.thr) ? 0.f : p.keep_scale;
           }
           ds[h2][r] = pr * (dp[r] * z - dlt);
@@ -838,8 +867,9 @@ void set_lds_attr(const void* fn, int bytes) {
 template <int D>
 void launch_fwd_v2(const AttnP& p, hipStream_t s) {
   const int lk_pad = (int)((p.Lk + 63) & ~63);
-  const int lds = 2 * lk_pad * AT<bf16, D>::RB;
-  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>), 2 * V2_LMAX * AT<bf16, D>::RB), true);
+  const int lds = 2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4;
+  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>),
+                                      2 * V2_LMAX * AT<bf16, D>::RB + V2_LMAX * 4), true);
   (void)once;
   hipLaunchKernelGGL((attn_fwd_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds, s, p);
 }
@@ -851,11 +881,12 @@ void launch_bwd_v2(const AttnP& p, hipStream_t s) {
   hipLaunchKernelGGL((attn_delta_kernel<bf16, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
   const int lq_pad = (int)((p.Lq + 31) & ~31), lk_pad = (int)((p.Lk + 31) & ~31);
   constexpr int NI1 = V2<D>::DUAL ? 2 : 4, NI2 = V2<D>::DUAL ? 2 : 3;  // LDS images per kernel
-  const int lds1 = NI1 * lq_pad * AT<bf16, D>::RB + 2 * V2_LMAX * 4;
-  const int lds2 = NI2 * lk_pad * AT<bf16, D>::RB;
+  const int lds1 = NI1 * lq_pad * AT<bf16, D>::RB + 3 * V2_LMAX * 4;
+  const int lds2 = NI2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4;
   static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<D>),
-                                      NI1 * V2_LMAX * AT<bf16, D>::RB + 2 * V2_LMAX * 4),
-                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>), NI2 * V2_LMAX * AT<bf16, D>::RB),
+                                      NI1 * V2_LMAX * AT<bf16, D>::RB + 3 * V2_LMAX * 4),
+                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>),
+                                      NI2 * V2_LMAX * AT<bf16, D>::RB + V2_LMAX * 4),
                       true);
   (void)once;
   hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_DKDV_THREADS), lds1, s, p);
