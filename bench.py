@@ -62,6 +62,74 @@ def pmc_traffic(kernel):
     return int(k["traffic_bytes_per_dispatch"]), os.path.basename(files[-1])
 
 
+def extract_main(args, dev, world, rank):
+    """BASELINE config 5: evidence-corpus build — ResNet50 image features (im2im_retrieval.py:29-36)
+    and MPNet CLS text embeddings at L=128 (text2text_retrieval.py:129-157), eval mode, random-init
+    weights, synthetic inputs resident in HBM; each rank processes its own shard (no collective).
+    A step = one batch of `--batch` images + `--batch` texts."""
+    from mmfd.encoders import MPNetConfig, MPNetModel
+    from mmfd.evidence import SentenceEncoder, resnet50
+
+    torch.manual_seed(42)
+    img = resnet50().to(dev).set_precision(args.precision)
+    enc = SentenceEncoder(MPNetModel(MPNetConfig()), device=dev, precision=args.precision)
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    px = torch.randn(args.batch, 3, 224, 224, generator=g).to(dev)
+    ids = torch.randint(3, 30527, (args.batch, 128), generator=g)
+    ids[:, 0] = 0
+    ids, mask = ids.to(dev), torch.ones_like(ids, device=dev)
+
+    def step():
+        f = img(px)
+        e = enc.encode_ids(ids, mask, batch_size=args.batch)
+        return f, e
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    t_img = t_txt = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0.record()
+        img(px)
+        e1.record()
+        enc.encode_ids(ids, mask, batch_size=args.batch)
+        e2.record()
+        e2.synchronize()
+        t_img += e0.elapsed_time(e1)
+        t_txt += e1.elapsed_time(e2)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    items = 2 * args.batch * world * args.steps
+    if rank == 0:
+        ips = args.batch * args.steps / (t_img * 1e-3)
+        tps = args.batch * args.steps / (t_txt * 1e-3)
+        out = {
+            "metric": "evidence-corpus items/sec (ResNet50 image features + MPNet L=128 text embeddings)",
+            "value": round(items / elapsed, 1), "unit": "items/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (random-init weights)",
+            "config": {"workload": "evidence corpus build (BASELINE config 5): resnet50 @224 + multi-qa-mpnet-base "
+                                   "@L=128, eval", "global_batch": args.batch * world, "parallelism": f"shard{world}"},
+            "images_per_s_per_gpu": round(ips, 1), "texts_per_s_per_gpu": round(tps, 1),
+            "image_tflops": round(ips * 8.174e9 / 1e12, 1), "text_tflops": round(tps * 22.35e9 / 1e12, 1),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -71,6 +139,7 @@ def main():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["train", "extract"], default="train")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,6 +159,8 @@ def main():
     from mmfd.train import build_flagship
 
     K.load()
+    if args.workload == "extract":
+        return extract_main(args, dev, world, rank)
     tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 

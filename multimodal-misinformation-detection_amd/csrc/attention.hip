@@ -541,10 +541,14 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   const float c2 = p.scale * LOG2E;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
+  uint4 qn[C::KCH];  // next query block's fragments, prefetched one block ahead
+  load_row_regs<T, D>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH];
-    load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+#pragma unroll
+    for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
+    load_row_regs<T, D>(qn, qb, p.q_st, q0 + V2_THREADS / 4 + li, p.Lq, lane, p.D);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
     const float* relrow = p.rel_bias ? p.rel_bias + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
