@@ -89,6 +89,28 @@ template <> struct V8<float> {
   }
 };
 
+// raw 16-B (bf16) / 32-B (fp32) holders for 8 consecutive elements, converted after all loads of a
+// pass are in flight
+template <typename TC> struct Raw8;
+template <> struct Raw8<bf16> {
+  uint4 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  }
+};
+template <> struct Raw8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const float4*>(p); b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+};
+
 // 8 consecutive columns [col, col+8) of one row; same operation order as epilogue_store
 template <typename TC>
 __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t ldc, int64_t N, int64_t row,
@@ -383,7 +405,8 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 // a counted vmcnt(6) in phase 3. The two wave rows run one barrier apart (ping-pong): while one
 // row issues its LDS reads and DMA the other row's MFMAs run.
 // =================================================================================================
-constexpr int G8_HALF = 16384, G8_LDS = 8 * G8_HALF;  // 2 buffers x 4 half-tiles = 128 KB
+constexpr int G8_HALF = 16384;
+constexpr int G8_LDS = 128 * (256 + 4) * 4;  // >= 2 buffers x 4 half-tiles (128 KB); 128-row epilogue staging
 constexpr int G8_BM = 256, G8_BN = 256, G8_BK = 64;
 
 __device__ __forceinline__ void g8_pre_barrier() {
@@ -557,15 +580,37 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     }
   }
 
-  // ---- epilogue: four passes of 64 rows (quadrant row mq = q >> 1 of wave row wr = q & 1)
+  if (alpha == 12345.0f) {  // EXPERIMENT: skip the epilogue (keep the accumulators alive)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+    return;
+  }
+  // ---- epilogue: two passes of 128 rows (quadrant row mq = pass); every wave stages its fp32
+  // accumulators, then all threads apply the epilogue to 8-column chunks with 16-B accesses
   constexpr int LDC = G8_BN + 4;
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
   const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
+  // fast path (full tile, 16-B aligned operands, no split-K slab): every thread owns the same 8
+  // columns in all its rows, so the bias is loaded once; per pass all residual / aux / C loads of
+  // the thread's 8 rows are issued before any math or store (one wait per pass, not per row)
+  if (!slab && e.vec && m0 + G8_BM <= M && n0 + G8_BN <= N) {
+    const int c8 = (tid % (G8_BN / 8)) * 8;
+    const int64_t col = n0 + c8;
+    float bia[8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (wr == (q & 1)) {
+    for (int u = 0; u < 8; ++u) bia[u] = e.bias ? e.bias[col + u] : 0.f;
+    const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
+    const bool fwd_act = e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU;
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq) {
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
@@ -574,11 +619,90 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              ct[(i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[q >> 1][nq][i][j][r];
+              ct[(wr * 64 + i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[mq][nq][i][j][r];
+      __syncthreads();
+      constexpr int IT = 128 * (G8_BN / 8) / NT;  // 8 rows per thread, in two groups of 4
+      constexpr int GI = 2;
+#pragma unroll
+      for (int k0 = 0; k0 < IT; k0 += GI) {
+      Raw8<TC> rres[GI], raux[GI], rc[GI];
+#pragma unroll
+      for (int k = 0; k < GI; ++k) {
+        const int64_t row = m0 + mq * 128 + tid / (G8_BN / 8) + (k0 + k) * (NT / (G8_BN / 8));
+        if (e.residual) rres[k].load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col);
+        if (bwd_act) raux[k].load(reinterpret_cast<const TC*>(e.aux) + row * e.ldaux + col);
+        if (e.beta != 0.f) rc[k].load(C + row * ldc + col);
+      }
+#pragma unroll
+      for (int k = 0; k < GI; ++k) {
+        const int lr = tid / (G8_BN / 8) + (k0 + k) * (NT / (G8_BN / 8));
+        const int64_t row = m0 + mq * 128 + lr;
+        const float* src = ct + lr * LDC + c8;
+        const float4 a4 = *reinterpret_cast<const float4*>(src), b4 = *reinterpret_cast<const float4*>(src + 4);
+        float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
+        float t[8];
+        if (e.residual && e.res_first) {
+          rres[k].get(t);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] += t[u];
+        }
+        if (fwd_act) {
+          if (e.aux) V8<TC>::store(reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col, z);
+          if (e.act == MMFD_ACT_GELU) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+          }
+        } else if (bwd_act) {
+          raux[k].get(t);
+          if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+          }
+        }
+        if (e.p > 0.f) {
+          const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)col;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
+        }
+        if (e.residual && !e.res_first) {
+          rres[k].get(t);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] += t[u];
+        }
+        if (e.beta != 0.f) {
+          rc[k].get(t);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+        }
+        V8<TC>::store(C + row * ldc + col, z);
+      }
+      }
+      __syncthreads();
     }
+    return;
+  }
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq) {
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(wr * 64 + i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[mq][nq][i][j][r];
     __syncthreads();
-    const int64_t rbase = m0 + (q >> 1) * 128 + (q & 1) * 64;
-    for (int idx = tid; idx < 64 * (G8_BN / 8); idx += NT) {
+    const int64_t rbase = m0 + mq * 128;
+    for (int idx = tid; idx < 128 * (G8_BN / 8); idx += NT) {
       const int lr = idx / (G8_BN / 8), c8 = (idx % (G8_BN / 8)) * 8;
       const int64_t row = rbase + lr, col = n0 + c8;
       if (row >= M || col >= N) continue;
@@ -587,6 +711,10 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
       float vv[8] = {alpha * a4.x, alpha * a4.y, alpha * a4.z, alpha * a4.w,
                      alpha * b4.x, alpha * b4.y, alpha * b4.z, alpha * b4.w};
       const bool full = col + 8 <= N;
+      if (alpha == 23456.0f) {  // EXPERIMENT: staging only, no global stores
+        asm volatile("" ::"v"(vv[0]), "v"(vv[3]), "v"(vv[7]));
+        continue;
+      }
       if (slab) {
         if (full && (N % 4) == 0) {
           *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(vv[0], vv[1], vv[2], vv[3]);
