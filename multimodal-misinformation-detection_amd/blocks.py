@@ -9,9 +9,27 @@ their gradients inside the GEMM epilogue).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import kernels as K
+
+_SIDE = {}
+
+
+def side_stream(device):
+    """Per-device stream for the weight-gradient GEMMs: they only depend on tensors the main
+    stream already produced, and nothing on the main stream reads their outputs until the layer's
+    gradients are reported (join), so they overlap with the data-gradient chain (dX GEMMs,
+    attention and LayerNorm backward). Opt-in (MMFD_SIDE_STREAM=1): with one 256x256 GEMM block
+    per CU the two streams only partition the CUs, and no gain was measured (1734 vs 1730 pairs/s)."""
+    if os.environ.get("MMFD_SIDE_STREAM", "0") != "1" or device.type != "cuda":
+        return None
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = _SIDE[device.index] = torch.cuda.Stream(device=device)
+    return s
 
 
 class StepCtx:
@@ -27,6 +45,18 @@ class StepCtx:
         self._written = set()
         self.grad_ready = None   # optional callable(names, grads): finished gradients (DP overlap)
         self._notified = set()
+        self.side = None         # stream for weight-gradient GEMMs (enable_side_stream)
+        self._side_used = False
+
+    def enable_side_stream(self, device):
+        self.side = side_stream(device)
+        return self
+
+    def join_side(self):
+        """main stream waits for every weight-gradient GEMM issued so far"""
+        if self.side is not None and self._side_used:
+            torch.cuda.current_stream().wait_stream(self.side)
+            self._side_used = False
 
     # ---- weights -------------------------------------------------------------------------------
     def w(self, name):
@@ -76,6 +106,7 @@ class StepCtx:
         """report the gradients written since the last call as final (a layer's backward is done)"""
         if self.grad_ready is None:
             return
+        self.join_side()
         names = [n for n in self.grads if n not in self._notified]
         if names:
             self._notified.update(names)
@@ -91,6 +122,16 @@ class StepCtx:
         return g, 1.0
 
     def lin_grads(self, names, dy2d, x2d):
+        if self.side is None:
+            return self._lin_grads(names, dy2d, x2d)
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            self._lin_grads(names, dy2d, x2d)
+        dy2d.record_stream(self.side)
+        x2d.record_stream(self.side)
+        self._side_used = True
+
+    def _lin_grads(self, names, dy2d, x2d):
         """dW = dy^T x (fp32, accumulate) with db = sum_rows(dy) fused into the same GEMM
         (a_rowsum); `names` are the row blocks of dy. A packed group (fused QKV / K|V) whose
         gradients are first written here is ONE GEMM into a packed buffer whose row blocks become
@@ -122,7 +163,7 @@ class StepCtx:
         r = 0
         for n in names:
             rows = self.P[n + ".weight"].shape[0]
-            self.lin_grads([n], dy2d[:, r:r + rows], x2d)
+            self._lin_grads([n], dy2d[:, r:r + rows], x2d)
             r += rows
 
 
@@ -149,10 +190,11 @@ def linear_packed(ctx: StepCtx, x2d, names):
     return K.gemm(x2d, W, bias=b)
 
 
-def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None):
+def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
+              residual=None):
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
     return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
-                  **(ctx.drop(drop_site) if drop_site else {}))
+                  residual=residual, **(ctx.drop(drop_site) if drop_site else {}))
 
 
 # -------------------------------------------------------------------------------------------------

@@ -176,8 +176,10 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         ctx.lin_grads([p + ".output.dense"], g2, f)
         dpre = Bk.linear_dx(ctx, g2, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre)
         ctx.lin_grads([p + ".intermediate.dense"], dpre, h1)
-        Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", out=ds2, beta=1.0)  # dh1
-        ds1, ds1d = Bk.layernorm_bwd(ctx, ds2, s1, p + ".attention.output.LayerNorm", m1, r1, drop_site=s + ".attn_out")
+        # dh1 = ds2 + dpre W (a fresh buffer: the weight-gradient GEMM on the side stream may still be
+        # reading ds2)
+        dh1 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", residual=ds2)
+        ds1, ds1d = Bk.layernorm_bwd(ctx, dh1, s1, p + ".attention.output.LayerNorm", m1, r1, drop_site=s + ".attn_out")
         g1 = ds1d if ds1d is not None else ds1
         ctx.lin_grads([p + ".attention.output.dense"], g1, Bk.as2d(o))
         do = Bk.linear_dx(ctx, g1, p + ".attention.output.dense").view(o.shape)
@@ -188,8 +190,7 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         dq2 = Bk.as2d(dqkv)
         ctx.lin_grads(names, dq2, x)
         Wp, _ = ctx.w_packed(names)
-        Bk.linear_dx(ctx, dq2, Wp, out=ds1, beta=1.0)  # dx_in
-        dx = ds1
+        dx = Bk.linear_dx(ctx, dq2, Wp, residual=ds1)  # dx_in = ds1 + dQKV [Wq;Wk;Wv] (fresh buffer)
         ctx.flush_ready()
     # embeddings: undo the embedding dropout, LayerNorm backward, scatter into the tables
     if st["emb_drop"]:
@@ -233,7 +234,9 @@ class _BertFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, dout):
         sc = fctx.sc
+        sc.enable_side_stream(dout.device)
         bert_backward(sc, fctx.model.config, dout.to(sc.dt), fctx.st, fctx.ids, fctx.tts)
+        sc.join_side()
         grads = [sc.grads.get(n) for n in fctx.names]
         fctx.sc = fctx.st = None
         return (None, None, None, None, None, None, *grads)
@@ -385,7 +388,9 @@ class _ViTFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, dout):
         sc = fctx.sc
+        sc.enable_side_stream(dout.device)
         vit_backward(sc, fctx.model.config, dout.to(sc.dt), fctx.st)
+        sc.join_side()
         sc.grads[PATCH_W] = sc.grads[PATCH_W].view(fctx.wshape)
         grads = [sc.grads.get(n) for n in fctx.names]
         fctx.sc = fctx.st = None
