@@ -253,8 +253,12 @@ class GemmProbe:
 
 
 def _kernel_name(a, split):
+    """the device kernel mmfd_gemm launches for these arguments (rocprof's demangled name)"""
     t = {F32: "float", BF16: "__bf16"}
-    base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
+    if a.dtype == BF16:  # 256x256 kernel (gemm.hip use_g8)
+        base = f"gemm256_kernel<{a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
+    else:
+        base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")
 
 
