@@ -56,7 +56,8 @@ def _worker(rank, world, port, bucket_mb, q):
         hook(["0.weight", "0.bias"], grads)
         dp.finish()
         res += [p.grad.clone() for p in m.parameters()]
-        q.put((rank, res))
+        # plain numpy: torch tensors travel as shared-memory fds that vanish when the worker exits
+        q.put((rank, [r.numpy() if r is not None else None for r in res]))
     finally:
         dist.destroy_process_group()
 
@@ -70,6 +71,7 @@ def test_grad_allreduce_gloo_world2(bucket_mb):
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
+    res = {k: [torch.from_numpy(a) if a is not None else None for a in v] for k, v in res.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
