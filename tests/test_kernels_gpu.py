@@ -133,6 +133,41 @@ def test_gemm_epilogues(dtype):
     _close(gy, (x.double() @ w.double().T) * t.grad, dtype, 1.0)
 
 
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("Kd", [64, 96, 768])
+def test_gemm_bf16_persistent_many_items(layout, Kd):
+    """The persistent 256x256 bf16 kernel walks several output tiles per workgroup as one K-tile
+    stream (more tiles than CUs; ragged last row/column tiles; K of one, two and twelve K-tiles),
+    with the bias + GELU + aux register epilogue. Reference: fp64 matmul on the GPU."""
+    M, N = 8192 + 136, 2304 + 40
+    g = torch.Generator(device=DEV).manual_seed(40)
+    x = torch.randn(M, Kd, device=DEV, generator=g).bfloat16()
+    w = torch.randn(N, Kd, device=DEV, generator=g).mul(0.1).bfloat16()
+    b = torch.randn(N, device=DEV, generator=g)
+    if layout == "nt":
+        ref = x.double() @ w.double().T
+        A, B, kw = x, w, {}
+    elif layout == "nn":  # B stored [K][N]
+        ref = x.double() @ w.double().T
+        A, B, kw = x, w.T.contiguous(), {"trans_b": True}
+    else:  # A stored [K][M], B stored [K][N]
+        ref = x.double() @ w.double().T
+        A, B, kw = x.T.contiguous(), w.T.contiguous(), {"trans_a": True, "trans_b": True}
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = K.gemm(A, B, bias=b, act=K.ACT_GELU, aux=aux, **kw)
+    pre = ref + b.double()
+    torch.cuda.synchronize()
+    e_aux = (aux.double() - pre).abs().max().item()
+    e_y = (y.double() - torch.nn.functional.gelu(pre)).abs().max().item()
+    scale = pre.abs().max().item()
+    assert e_aux <= 1e-2 * scale and e_y <= 1e-2 * scale, (e_aux, e_y, scale)
+    # fp32 output with residual, no activation
+    res = torch.randn(M, N, device=DEV, generator=g)
+    y32 = K.gemm(A, B, residual=res, out_dtype=torch.float32, **kw)
+    torch.cuda.synchronize()
+    assert (y32.double() - (ref + res.double())).abs().max().item() <= 1e-4 * scale
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_dropout_mask(dtype):
     M, N, Kd = 256, 128, 64
