@@ -29,7 +29,7 @@ extern "C" {
 
 typedef void* mmfd_stream_t; /* hipStream_t */
 
-enum { MMFD_F32 = 0, MMFD_BF16 = 1 };
+enum { MMFD_F32 = 0, MMFD_BF16 = 1, MMFD_F16 = 2 /* retrieval corpora only */ };
 enum {
   MMFD_ACT_NONE = 0,
   MMFD_ACT_GELU = 1,      /* exact erf GELU, nn.GELU() (layers.py:14) / HF "gelu" */
@@ -267,6 +267,30 @@ int mmfd_act_bwd(int dtype, int64_t n, const void* dy, const void* aux, int act,
                  const uint64_t* seed, uint64_t salt, void* out, mmfd_stream_t stream);
 /* seed[0] += 1 (advances the step seed inside a captured graph) */
 int mmfd_seed_advance(uint64_t* seed, mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* Evidence retrieval scoring.                                             */
+/* Replaces the per-image Python loop of ImageCorpus.retrieve_similar_images                    */
+/* (src/evidence/im2im_retrieval.py:80-92: nn.CosineSimilarity(dim=1, eps=1e-6) per corpus      */
+/* entry, then sorted(reverse=True) at :94-96) and the bi-encoder stage of                      */
+/* SemanticSimilarity.search (src/evidence/text2text_retrieval.py:49-66: util.semantic_search,  */
+/* i.e. cos_sim of normalised fp16 embeddings + top-k).                                         */
+/* cosine_scores: scores[q][n] (fp32, leading dim lds) for fp32 queries [Q][ldq] against a      */
+/*   corpus [N][ldc] of corpus_dtype (MMFD_F32 / MMFD_BF16 / MMFD_F16; 16-byte aligned rows,    */
+/*   D % 8 == 0). mode MMFD_COS_PAIR: dot / sqrt(max(|q|^2 |c|^2, eps^2)) (nn.CosineSimilarity); */
+/*   MMFD_COS_NORMALIZED: dot / (max(|q|, eps) max(|c|, eps)) (util.cos_sim, eps 1e-12); OR     */
+/*   MMFD_COS_ROUND_F16 to round each score to fp16 (scores of fp16 embeddings).               */
+/* topk: per query, the k largest scores in descending order, ties broken by the LOWER corpus   */
+/*   index (the order of Python's stable sort over the reference's insertion-ordered corpus);   */
+/*   k <= 2048; missing entries (k > N) are -inf / -1. Workspace from mmfd_topk_workspace_bytes.*/
+/* ------------------------------------------------------------------------------------------- */
+enum { MMFD_COS_PAIR = 0, MMFD_COS_NORMALIZED = 1, MMFD_COS_ROUND_F16 = 4 };
+int mmfd_cosine_scores(int corpus_dtype, int64_t Q, int64_t N, int64_t D, const float* queries,
+                       int64_t ldq, const void* corpus, int64_t ldc, int mode, float eps, float* scores,
+                       int64_t lds, mmfd_stream_t stream);
+int64_t mmfd_topk_workspace_bytes(int64_t Q, int64_t N, int64_t k);
+int mmfd_topk(int64_t Q, int64_t N, const float* scores, int64_t lds, int64_t k, float* out_val,
+              int64_t* out_idx, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -242,6 +242,23 @@ class ImageCorpus:
                 self.feature_dict[p] = f
         self.save_features()
 
+    def index(self):
+        """The corpus features as a device-resident CorpusIndex (rebuilt when the corpus changed)."""
+        from .retrieval import CorpusIndex
+        key = (len(self.feature_dict), next(reversed(self.feature_dict)) if self.feature_dict else None)
+        if getattr(self, "_index_key", None) != key:
+            paths = list(self.feature_dict)
+            feats = torch.stack([self.feature_dict[p].float().flatten() for p in paths])
+            self._index = CorpusIndex(feats, ids=paths, device=self.feature_extractor.device, mode="pair", eps=1e-6)
+            self._index_key = key
+        return self._index
+
+    def retrieve_similar_images(self, query_image_path, top_k=50):
+        """im2im_retrieval.py:80-106: [(path, score)] of the top_k corpus images with distinct
+        cosine scores, best first (scores and ranking on the GPU: retrieval.CorpusIndex)."""
+        q = self.feature_extractor.extract_features(query_image_path)
+        return self.index().search(q.float().unsqueeze(0).to(self.feature_extractor.device), top_k)[0]
+
 
 # -------------------------------------------------------------------------------------------------
 # text corpus (text2text_retrieval.py:123-157)

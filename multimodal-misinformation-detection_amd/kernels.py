@@ -16,7 +16,8 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmmfd_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
+COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
 
 
@@ -125,6 +126,9 @@ SIGNATURES = {
     "mmfd_dropout": (_I, [_I, _I64, _VP, _VP, _F, _VP, _U64, _VP]),
     "mmfd_seed_advance": (_I, [_VP, _VP]),
     "mmfd_act_bwd": (_I, [_I, _I64, _VP, _VP, _I, _F, _VP, _U64, _VP, _VP]),
+    "mmfd_cosine_scores": (_I, [_I, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I, _F, _VP, _I64, _VP]),
+    "mmfd_topk_workspace_bytes": (_I64, [_I64, _I64, _I64]),
+    "mmfd_topk": (_I, [_I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _I64, _VP]),
 }
 
 _lib = None
@@ -674,3 +678,43 @@ def adamw(table_dev, n, max_numel, lr, beta1, beta2, eps, weight_decay):
 
 def dropout_hash(seed: int, salt: int, index: int) -> int:
     return int(lib().mmfd_dropout_hash(seed & 0xFFFFFFFFFFFFFFFF, salt & 0xFFFFFFFFFFFFFFFF, index))
+
+
+# ------------------------------------------------------------------------------------------------
+# retrieval scoring (csrc/retrieval.hip)
+# ------------------------------------------------------------------------------------------------
+_CORPUS_CODES = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+
+
+def cosine_scores(queries, corpus, mode=COS_PAIR, eps=1e-6, out=None):
+    """fp32 [Q, N] cosine scores of fp32 queries [Q, D] against a corpus [N, D] (fp32 / bf16 / fp16)."""
+    _require_cuda(queries, corpus, out)
+    if queries.dim() == 1:
+        queries = queries.unsqueeze(0)
+    queries = queries.float().contiguous()
+    corpus = corpus.contiguous()
+    Q, D = queries.shape
+    N = corpus.shape[0]
+    if corpus.shape[1] != D:
+        raise ValueError(f"query dim {D} != corpus dim {corpus.shape[1]}")
+    if corpus.dtype not in _CORPUS_CODES:
+        raise TypeError(f"unsupported corpus dtype {corpus.dtype}")
+    if out is None:
+        out = torch.empty(Q, N, device=corpus.device, dtype=torch.float32)
+    _check(lib().mmfd_cosine_scores(_CORPUS_CODES[corpus.dtype], Q, N, D, _ptr(queries), D, _ptr(corpus), _ld(corpus),
+                                    int(mode), float(eps), _ptr(out), _ld(out), _stream()), "mmfd_cosine_scores")
+    return out
+
+
+def topk(scores, k):
+    """Per row of fp32 scores [Q, N]: the k largest, descending, ties -> lower index first.
+    Returns (values fp32 [Q, k], indices int64 [Q, k]); missing entries are -inf / -1."""
+    _require_cuda(scores)
+    Q, N = scores.shape
+    val = torch.empty(Q, k, device=scores.device, dtype=torch.float32)
+    idx = torch.empty(Q, k, device=scores.device, dtype=torch.int64)
+    nbytes = lib().mmfd_topk_workspace_bytes(Q, N, k)
+    ws = torch.empty(max(nbytes, 8), device=scores.device, dtype=torch.uint8)
+    _check(lib().mmfd_topk(Q, N, _ptr(scores), _ld(scores), k, _ptr(val), _ptr(idx), _ptr(ws), nbytes, _stream()),
+           "mmfd_topk")
+    return val, idx

@@ -177,3 +177,32 @@ def test_extractor_state_dict_names():
     ref = {k[len("param/"):]: tuple(zm[k].shape) for k in zm.files if k.startswith("param/")}
     ref.pop("embeddings.position_ids", None)
     assert mine == ref
+
+
+# ---- retrieval scoring (§8(f) row 2) -----------------------------------------------------------------
+def test_oracle_retrieval_cosine_matches_torch_modules():
+    """oracle/retrieval.py restates nn.CosineSimilarity(dim=1, eps=1e-6) (the module
+    im2im_retrieval.py:40 calls per corpus image) and util.cos_sim's F.normalize(eps=1e-12) form;
+    pinned here against torch's own CPU implementations of both."""
+    from oracle.retrieval import cosine_normalized, cosine_pair
+    g = torch.Generator().manual_seed(3)
+    q = torch.randn(3, 64, generator=g)
+    c = torch.randn(50, 64, generator=g)
+    c[7] = 0.0  # zero row: the eps clamp decides
+    cos = torch.nn.CosineSimilarity(dim=1, eps=1e-6)
+    ref = torch.stack([torch.stack([cos(q[i:i + 1].double(), c[j:j + 1].double())[0] for j in range(50)]) for i in range(3)])
+    np.testing.assert_allclose(cosine_pair(q.numpy(), c.numpy()), ref.numpy(), rtol=1e-12, atol=1e-12)
+    fn = torch.nn.functional.normalize
+    ref2 = fn(q.double(), p=2, dim=1) @ fn(c.double(), p=2, dim=1).T
+    np.testing.assert_allclose(cosine_normalized(q.numpy(), c.numpy()), ref2.numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_oracle_retrieval_order_and_distinct_filter():
+    """sorted(..., key=score, reverse=True) keeps corpus order among equal scores, and the
+    reference's filter keeps the first entry of every distinct score (im2im_retrieval.py:94-106)"""
+    from oracle.retrieval import ranked, retrieve_unique
+    s = np.array([0.5, 0.9, 0.5, 0.9, 0.1, 0.7, 0.9])
+    items = sorted({i: float(v) for i, v in enumerate(s)}.items(), key=lambda x: x[1], reverse=True)
+    assert [i for i, _ in items] == list(ranked(s))
+    assert retrieve_unique(s, 3) == [(1, 0.9), (5, 0.7), (0, 0.5)]
+    assert retrieve_unique(s, 10) == [(1, 0.9), (5, 0.7), (0, 0.5), (4, 0.1)]
