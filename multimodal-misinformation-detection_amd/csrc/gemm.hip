@@ -173,12 +173,16 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
 // ds_read_b64_tr_b16 with 8-B unit u of row r at u ^ 4*((r&3) | ((r>>3)&1)<<2) (conflict-free tr
 // reads), fp32 fragments from 4 ds_read_b32 with chunk c at c ^ 4*((r>>2)&1).
 // -------------------------------------------------------------------------------------------------
-template <typename T, int LAYOUT, int MNW>
+// SW = 1 (layout 0 only): the B image of the 256x256 kernel, whose fragments gather rows
+// 8p + 4j + (0..3) (see g8_load_b); chunk c of row r at c ^ (2*((r>>1)&1) | 4*((r>>3)&1)) keeps
+// those ds_read_b128 reads conflict-free.
+template <typename T, int LAYOUT, int MNW, int SW = 0>
 struct Img {
   static constexpr int RBY = LAYOUT == 0 ? ROWB : MNW * (int)sizeof(T);  // bytes per image row
   static constexpr int CPR = RBY / 16;                                    // 16-B chunks per row
   static constexpr int RPI = 1024 / RBY;                                  // rows per 1-KB DMA piece
   __device__ __forceinline__ static int swz(int r, int c) {  // physical chunk <-> logical chunk
+    if (LAYOUT == 0 && SW == 1) return c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2));
     if (LAYOUT == 0) return c ^ (r & 7);
     if (sizeof(T) == 2) return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
     return c ^ (4 * ((r >> 2) & 1));
@@ -211,11 +215,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, 
 // One operand's share of a stage fill: NP 1-KB LDS-DMA pieces per wave (buffer_load ... lds). The
 // per-lane source offsets are loop invariant (the K tile advances through soffset) and chunks
 // outside the matrix point past num_records, so the DMA writes zeros there.
-template <typename T, int LAYOUT, int MNW, int NP>
+template <typename T, int LAYOUT, int MNW, int NP, int SW = 0>
 struct Fill {
   uint32_t off[NP];
   __device__ __forceinline__ void init(int64_t ld, int64_t mn0, int64_t mn_ext, int wave, int lane) {
-    using I = Img<T, LAYOUT, MNW>;
+    using I = Img<T, LAYOUT, MNW, SW>;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       const int q = wave * NP + j;                     // piece index within the image
@@ -230,7 +234,7 @@ struct Fill {
   }
   __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, uint32_t soff, bool tail, int64_t k0,
                                         int64_t K, int wave, int lane) {
-    using I = Img<T, LAYOUT, MNW>;
+    using I = Img<T, LAYOUT, MNW, SW>;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       uint32_t o = off[j];
@@ -427,12 +431,35 @@ __device__ __forceinline__ void g8_frag_a(uint4 (&a)[4][2], const char* img, int
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<bf16, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
 }
+// B fragment j (j = 0, 1) of the wave's 32 columns gathers the 4-column units 2p + j (p = 0..3),
+// and the MFMA runs with swapped operands (acc = B-fragment x A-fragment = the C^T block): lane
+// (g, ci) of accumulator (i, j) then holds row i*16 + ci, columns 8g + 4j .. +3, i.e. every lane
+// owns 8 CONSECUTIVE columns of a row (fragment 0 the low four) — one 16-byte bf16 chunk for the
+// register epilogue. The K-contiguous B image uses the SW = 1 swizzle under which these
+// ds_read_b128 are conflict-free; the MN-contiguous (transposed ds_read_b64_tr_b16) B reads are
+// 2-way (each 16-B chunk is read in one half only), well inside the LDS budget of a K-tile.
+template <int LAYOUT>
+__device__ __forceinline__ uint4 g8_load_b(const char* img, int wc, int j, int kc, int lane) {
+  using I = Img<bf16, LAYOUT, 128, 1>;
+  const int g = lane >> 4, i = lane & 15;
+  if (LAYOUT == 0) {
+    const int row = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
+    return lds_read16(img, row * ROWB + (I::swz(row, kc * 4 + g) << 4));
+  } else {
+    const int q = i >> 2, p = i & 3;
+    const int r1 = kc * 32 + 8 * g + q, r2 = r1 + 4;
+    const int u = wc * 8 + 2 * p + j;  // 8-B unit (4 bf16)
+    const uint2 a = lds_read_tr16(img + r1 * I::RBY + (I::swz(r1, u >> 1) << 4) + ((u & 1) << 3));
+    const uint2 b = lds_read_tr16(img + r2 * I::RBY + (I::swz(r2, u >> 1) << 4) + ((u & 1) << 3));
+    return make_uint4(a.x, a.y, b.x, b.y);
+  }
+}
 template <int LAYOUT>
 __device__ __forceinline__ void g8_frag_b(uint4 (&b)[2][2], const char* img, int wc, int lane) {
 #pragma unroll
   for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j][kc] = load_frag<bf16, LAYOUT, 128>(img, wc * 2 + j, kc, lane);
+    for (int j = 0; j < 2; ++j) b[j][kc] = g8_load_b<LAYOUT>(img, wc, j, kc, lane);
 }
 __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2], const uint4 (&b)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
@@ -441,7 +468,7 @@ __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) Mma<bf16>::run(acc[i][j], a[i][kc], b[j][kc]);
+      for (int j = 0; j < 2; ++j) Mma<bf16>::run(acc[i][j], b[j][kc], a[i][kc]);
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -489,7 +516,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * 2);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * 2);
   Fill<bf16, TA, 128, 2> fa0, fa1;
-  Fill<bf16, TB, 128, 2> fb0, fb1;
+  Fill<bf16, TB, 128, 2, 1> fb0, fb1;
   fa0.init(lda, m0, M, wave, lane);
   fa1.init(lda, m0 + 128, M, wave, lane);
   fb0.init(ldb, n0, N, wave, lane);
@@ -617,9 +644,8 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              ct[(wr * 64 + i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[mq][nq][i][j][r];
+            *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+                acc[mq][nq][i][j];
       __syncthreads();
       constexpr int IT = 128 * (G8_BN / 8) / NT;  // 8 rows per thread, in two groups of 4
       constexpr int GI = 2;
@@ -697,9 +723,8 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ct[(wr * 64 + i * 16 + 4 * g + r) * LDC + nq * 128 + wc * 32 + j * 16 + ci] = acc[mq][nq][i][j][r];
+          *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+              acc[mq][nq][i][j];
     __syncthreads();
     const int64_t rbase = m0 + mq * 128;
     for (int idx = tid; idx < 128 * (G8_BN / 8); idx += NT) {
