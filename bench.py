@@ -4,7 +4,7 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|extract|retrieve]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve]
 """
 import argparse
 import json
@@ -212,6 +212,50 @@ def retrieve_main(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def forward_main(args, dev, world, rank):
+    """BASELINE config 2: bert-base-uncased + ViT-B/16 + fusion head forward only (eval), default
+    bs=64 pairs per GPU, synthetic pairs resident in HBM; a step = one batch of pairs.
+    Logit parity for this path: tests/test_trainer_gpu.py::test_config2_full_size_forward_logits."""
+    from mmfd import kernels as K  # noqa: F401
+    from mmfd.dataset import synthetic_batch
+    from mmfd.train import build_flagship
+
+    tr = build_flagship(dev, args.precision, seed=42 + rank)
+    batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
+    for _ in range(args.warmup):
+        tr.predict(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.predict(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    if rank == 0:
+        pairs = args.batch * world * args.steps / elapsed
+        tf = pairs / world * 117.21e9 / 1e12  # SURVEY 8(d) config 2: 117.21 GFLOP/pair forward
+        out = {"metric": "claim-evidence pairs/sec (forward only, eval)", "value": round(pairs, 2), "unit": "pairs/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": args.precision, "data": "synthetic (Factify-shaped pairs, random-init weights)",
+               "config": {"workload": "config 2: bert-base-uncased + ViT-B/16 + fusion head forward (eval)",
+                          "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
+                          "parallelism": f"dp{world}"},
+               "step_tflops_per_gpu": round(tf, 1), "step_mfma_frac": round(tf / PEAK_TFLOPS[args.precision], 4)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,7 +265,7 @@ def main():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["train", "extract", "retrieve"], default="train")
+    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve"], default="train")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -245,6 +289,8 @@ def main():
         return extract_main(args, dev, world, rank)
     if args.workload == "retrieve":
         return retrieve_main(args, dev, world, rank)
+    if args.workload == "forward":
+        return forward_main(args, dev, world, rank)
     tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 

@@ -91,6 +91,25 @@ class FusionTrainer:
         return loss
 
 
+    @torch.no_grad()
+    def predict(self, batch):
+        """Dual-encoder + fusion forward in eval mode (BASELINE config 2; the inference of
+        evaluate.py:112-164 with batched pairs): ((y_tt, y_ti), (y_it, y_ii)) for claim =
+        batch[:B], evidence = batch[B:] of the stacked encoder inputs."""
+        mods = (self.text_encoder, self.image_encoder, self.head)
+        was = [m.training for m in mods]
+        for m in mods:
+            m.eval()
+        try:
+            B = batch["pixel_values"].shape[0] // 2
+            T = self.text_encoder(input_ids=batch["input_ids"], attention_mask=batch["attention_mask"]).last_hidden_state
+            I = self.image_encoder(batch["pixel_values"]).last_hidden_state
+            return self.head(T[:B], I[:B], T[B:], I[B:])
+        finally:
+            for m, w in zip(mods, was):
+                m.train(w)
+
+
 def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders=False, lr=1e-4, dp=None,
                    seed=42):
     """bert-base-uncased + ViT-B/16 + the fusion head at 768/768 (BASELINE configs 2-4), random init."""

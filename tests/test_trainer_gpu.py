@@ -42,3 +42,33 @@ def test_frozen_encoders_only_head_updates():
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(before, tr.text_encoder.parameters()))
     assert any(not torch.equal(a, b) for a, b in zip(hb, tr.head.parameters()))
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 5e-2)])
+def test_config2_full_size_forward_logits(precision, tol):
+    """BASELINE config 2 at full size: bert-base-uncased + ViT-B/16 + the fusion head (768/768,
+    E=256, H=8), eval-mode forward of claim/evidence pairs (ragged text masks), logits vs the CPU
+    oracle (oracle/encoders.py + oracle/fusion_head.py). Tolerance: north_star's 1e-3 abs in fp32;
+    5e-2 abs in bf16 (SURVEY 7 "Hard parts": bf16 moves logits by up to 1.8e-2)."""
+    from mmfd.train import build_flagship
+    from oracle import encoders as OE
+    from oracle import fusion_head as OF
+    from mmfd.dataset import synthetic_batch
+
+    tr = build_flagship("cuda", precision, dropout=0.1, seed=3)
+    B = 2
+    batch = synthetic_batch(B, seed=17, device="cpu", ragged=True)
+    out = tr.predict({k: v.cuda() for k, v in batch.items()})
+    torch.cuda.synchronize()
+    sd = lambda m: {k: v.detach().float().cpu() for k, v in m.state_dict().items()}  # noqa: E731
+    bp, vp, hp = sd(tr.text_encoder), sd(tr.image_encoder), sd(tr.head)
+    with torch.no_grad():
+        T = OE.bert_forward(bp, batch["input_ids"], batch["attention_mask"], None, num_layers=12, num_heads=12)
+        I = OE.vit_forward(vp, batch["pixel_values"], num_layers=12, num_heads=12, patch=16)
+        ref = OF.model_forward(hp, T[:B], I[:B], T[B:], I[B:], num_heads=8)
+    got = [y for pair in out for y in pair]
+    want = [y for pair in ref for y in pair]
+    for g, w in zip(got, want):
+        assert g.shape == w.shape
+        err = (g.float().cpu() - w).abs().max().item()
+        assert err < tol, (precision, err)
