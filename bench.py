@@ -4,7 +4,7 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess]
 """
 import argparse
 import json
@@ -256,6 +256,74 @@ def forward_main(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def preprocess_main(args, dev, world, rank):
+    """raw-image preprocessing (dataset.py:14-19 transform: Resize(256) +
+    CenterCrop(256) + ToTensor + Normalize) of `--batch` decoded 375x500 RGB images already in
+    HBM -> the fp32 [B, 3, 256, 256] pixel tensor; bit-exact with PIL + torchvision
+    (tests/test_preprocess_gpu.py). Each rank processes its own images (no collective)."""
+    from mmfd.preprocess import ImagePreprocessor
+
+    H, W = 375, 500
+    pre = ImagePreprocessor("train", device=dev)
+    g = torch.Generator(device="cpu").manual_seed(5 + rank)
+    src = torch.randint(0, 256, (args.batch, H, W, 3), generator=g, dtype=torch.uint8).to(dev)
+    plan = pre.plan([(H, W)] * args.batch, [src[i].data_ptr() for i in range(args.batch)])
+    out = torch.empty(args.batch, 3, 256, 256, device=dev)
+    for _ in range(args.warmup):
+        pre.launch(plan, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        pre.launch(plan, out)
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    if rank == 0:
+        per = e0.elapsed_time(e1) / args.steps * 1e-3
+        oh, ow = 256, 341
+        # algorithmic bytes per image: source read, pass-1 rows written + read, fp32 output written
+        algo = H * W * 3 + 2 * H * ow * 3 + 3 * 256 * 256 * 4
+        achieved = algo * args.batch / per / 1e9
+        out_d = {"metric": "images/sec preprocessed (Resize 256 + CenterCrop 256 + ToTensor + Normalize)",
+                 "value": round(args.batch * world * args.steps / elapsed, 1), "unit": "images/s", "n_gpus": world,
+                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                 "data": "synthetic 375x500 RGB uint8 images resident in HBM",
+                 "config": {"workload": "raw-image preprocessing (SURVEY 8f row 3), dataset.py:14-19 transform",
+                            "global_batch": args.batch * world, "parallelism": f"shard{world}"},
+                 "roofline": {"bound": "hbm", "kernel": "resize_h_kernel + resize_v_norm_kernel",
+                              "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                              "frac": round(achieved / 8000.0, 4), "traffic": None,
+                              "algorithmic_bytes_per_launch": algo * args.batch, "avg_launch_us": round(per * 1e6, 2)}}
+        if not args.no_cpu_baseline and world == 1:
+            from PIL import Image
+            from oracle.preprocess import preprocess
+            from mmfd.preprocess import MODES
+            c = MODES["train"]
+            imgs = [Image.fromarray(src[i].cpu().numpy()) for i in range(min(32, args.batch))]
+            t1 = time.perf_counter()
+            for im in imgs:
+                preprocess(im, c["resize"], c["crop"], c["mean"], c["std"])
+            dt = (time.perf_counter() - t1) / len(imgs)
+            out_d["cpu_baseline"] = {"value": round(1.0 / dt, 1), "unit": "images/s", "cores": 1, "kind": "port",
+                                     "sample": f"oracle/preprocess.py (PIL resize + numpy normalise), {len(imgs)} images, one thread"}
+        print(json.dumps(out_d), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,7 +333,7 @@ def main():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve"], default="train")
+    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess"], default="train")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -291,6 +359,8 @@ def main():
         return retrieve_main(args, dev, world, rank)
     if args.workload == "forward":
         return forward_main(args, dev, world, rank)
+    if args.workload == "preprocess":
+        return preprocess_main(args, dev, world, rank)
     tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 

@@ -292,6 +292,28 @@ int64_t mmfd_topk_workspace_bytes(int64_t Q, int64_t N, int64_t k);
 int mmfd_topk(int64_t Q, int64_t N, const float* scores, int64_t lds, int64_t k, float* out_val,
               int64_t* out_idx, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------- */
+/* Raw-image preprocessing: PIL bilinear resize (as torchvision's Resize on */
+/* PIL images: src/model/dataset.py:14-19 Resize(256)+CenterCrop(256), and                     */
+/* src/evidence/im2im_retrieval.py:19-27 Resize((224,224))) + crop + ToTensor + Normalize, for a */
+/* batch of decoded RGB uint8 HWC images already on the device. The host supplies PIL's taps:   */
+/* coef holds, per image and axis, one record [xmin, n, k_0 .. k_{K-1}] (int32, 22-bit fixed    */
+/* point, K = kx_size / ky_size) per output position; the result is bit-identical to PIL +      */
+/* torchvision. out: fp32 [n_images][3][Ho][Wo]; the crop window starts at (crop_y, crop_x) of  */
+/* the resized (out_h x out_w) image. workspace: per image h * out_w * 3 bytes at tmp_off.      */
+/* mean3 / std3 are HOST arrays of 3 floats.                                                    */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct mmfd_image_desc {
+  const uint8_t* src; int64_t h, w, stride;  /* device pointer, rows of stride bytes, RGB      */
+  int32_t out_h, out_w, crop_y, crop_x;      /* resized size and crop origin                  */
+  int64_t kx_off, ky_off;                    /* int32 offsets of the x / y tap tables in coef */
+  int32_t kx_size, ky_size;                  /* taps per record (K)                           */
+  int64_t tmp_off;                           /* byte offset of the image's pass-1 rows        */
+} mmfd_image_desc;
+int mmfd_resize_normalize(int64_t n_images, const mmfd_image_desc* descs, int64_t max_h, int64_t max_out_w,
+                          const int32_t* coef, void* workspace, int64_t Ho, int64_t Wo, const float* mean3,
+                          const float* std3, float* out, mmfd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -129,6 +129,8 @@ SIGNATURES = {
     "mmfd_cosine_scores": (_I, [_I, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I, _F, _VP, _I64, _VP]),
     "mmfd_topk_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "mmfd_topk": (_I, [_I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _I64, _VP]),
+    "mmfd_resize_normalize": (_I, [_I64, _VP, _I64, _I64, _VP, _VP, _I64, _I64, ctypes.POINTER(ctypes.c_float),
+                                   ctypes.POINTER(ctypes.c_float), _VP, _VP]),
 }
 
 _lib = None

@@ -206,3 +206,51 @@ def test_oracle_retrieval_order_and_distinct_filter():
     assert [i for i, _ in items] == list(ranked(s))
     assert retrieve_unique(s, 3) == [(1, 0.9), (5, 0.7), (0, 0.5)]
     assert retrieve_unique(s, 10) == [(1, 0.9), (5, 0.7), (0, 0.5), (4, 0.1)]
+
+
+# ---- raw-image preprocessing (§8(f) row 3) ------------------------------------------------------------
+def _resample_with_taps(a, oh, ow):
+    """PIL's two-pass 8-bit integer resample driven by mmfd.preprocess.pil_taps (host logic under
+    test: the taps the GPU kernels consume)"""
+    from mmfd.preprocess import pil_taps
+    tx, ty = pil_taps(a.shape[1], ow).astype(np.int64), pil_taps(a.shape[0], oh).astype(np.int64)
+    tmp = np.zeros((a.shape[0], ow, 3), np.int64)
+    for xx in range(ow):
+        x0, n = tx[xx, 0], tx[xx, 1]
+        s = (1 << 21) + (a[:, x0:x0 + n, :].astype(np.int64) * tx[xx, 2:2 + n][None, :, None]).sum(1)
+        tmp[:, xx] = np.clip(s >> 22, 0, 255)
+    out = np.zeros((oh, ow, 3), np.int64)
+    for yy in range(oh):
+        y0, n = ty[yy, 0], ty[yy, 1]
+        s = (1 << 21) + (tmp[y0:y0 + n] * ty[yy, 2:2 + n][:, None, None]).sum(0)
+        out[yy] = np.clip(s >> 22, 0, 255)
+    return out.astype(np.uint8)
+
+
+@pytest.mark.parametrize("h,w,oh,ow", [(375, 500, 256, 341), (480, 640, 224, 224), (100, 90, 224, 224),
+                                       (256, 300, 256, 300), (257, 1000, 224, 224), (31, 7, 256, 57)])
+def test_pil_taps_reproduce_pil_resize_exactly(h, w, oh, ow):
+    from PIL import Image
+    a = np.random.default_rng(h * w).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    ref = np.asarray(Image.fromarray(a).resize((ow, oh), Image.BILINEAR))
+    assert np.array_equal(_resample_with_taps(a, oh, ow), ref)
+
+
+def test_preprocess_oracle_matches_torch_tensor_ops_and_size_rules():
+    """oracle/preprocess.py's ToTensor/Normalize arithmetic equals torch's fp32 CPU ops bit for bit;
+    the torchvision size / crop rules (Resize(int) keeps the aspect ratio with a truncated long
+    side, CenterCrop rounds the origin with Python's round) on known cases"""
+    from PIL import Image
+    from oracle.preprocess import preprocess, resized_size
+    from mmfd.preprocess import center_crop_origin, resized_size as host_size
+    assert resized_size(375, 500, 256) == (256, 341) and resized_size(500, 375, 256) == (341, 256)
+    assert resized_size(256, 999, 256) == (256, 999) and resized_size(10, 20, (224, 224)) == (224, 224)
+    for hw in [(375, 500), (500, 375), (256, 257), (100, 90), (999, 256)]:
+        assert host_size(*hw, 256) == resized_size(*hw, 256)
+    assert center_crop_origin(256, 341, 256) == (0, 42) and center_crop_origin(257, 256, 256) == (0, 0)
+    a = np.random.default_rng(1).integers(0, 256, (300, 400, 3), dtype=np.uint8)
+    got = preprocess(Image.fromarray(a), (224, 224), None, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225))
+    img = np.asarray(Image.fromarray(a).resize((224, 224), Image.BILINEAR))
+    t = torch.from_numpy(img.copy()).permute(2, 0, 1).contiguous().to(torch.float32).div(255)
+    t = t.sub_(torch.tensor([0.485, 0.456, 0.406])[:, None, None]).div_(torch.tensor([0.229, 0.224, 0.225])[:, None, None])
+    assert np.array_equal(got, t.numpy())
