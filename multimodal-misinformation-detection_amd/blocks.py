@@ -32,10 +32,27 @@ def side_stream(device):
     return s
 
 
+# Persistent compute-dtype copies of the fp32 master weights ("shadows"). A module keeps its
+# shadows across steps (`shadow_store(module)`: key -> (bf16 tensor, [(param name, data_ptr,
+# version)])); SHADOW_OF maps a master parameter's data_ptr to the bf16 view that mmfd.optim.AdamW
+# refreshes in the same kernel that updates the parameter (mmfd_adamw's param_bf16), so the
+# weights are cast once, not once per step. Any other in-place update of a parameter (load_state_dict,
+# torch optimizers, manual edits) bumps its version counter, and the shadow is re-cast.
+SHADOW_OF = {}
+
+
+def shadow_store(module):
+    st = module.__dict__.get("_mmfd_shadows")
+    if st is None:
+        st = module.__dict__["_mmfd_shadows"] = {}
+    return st
+
+
 class StepCtx:
     def __init__(self, params: dict, dtype: torch.dtype, dropout_p: float = 0.0, seed: K.Seed | None = None,
-                 training: bool = False):
+                 training: bool = False, shadows: dict | None = None):
         self.P = params          # name -> fp32 master tensor (nn.Parameter data)
+        self.shadows = shadows   # persistent shadow store of the owning module (see SHADOW_OF)
         self.dt = dtype
         self.p = float(dropout_p) if training else 0.0
         self.seed = seed
@@ -59,13 +76,53 @@ class StepCtx:
             self._side_used = False
 
     # ---- weights -------------------------------------------------------------------------------
+    def _shadow(self, key, pnames):
+        """the persistent compute-dtype copy of the row-concatenated weights `pnames`, or None when
+        it has to be (re)built (absent, a master weight changed outside mmfd's AdamW, or a weight
+        already shadowed under another key)"""
+        if self.shadows is None:
+            return None
+        ent = self.shadows.get(key)
+        if ent is None:
+            return None
+        t, members = ent
+        for n, ptr, ver in members:
+            src = self.P[n]
+            if src.data_ptr() != ptr or src._version != ver or SHADOW_OF.get(ptr) is None:
+                return None
+        return t
+
+    def _register(self, key, t, pnames):
+        """record `t` (rows of the weights `pnames`) as their shadow when none of them has one yet"""
+        if self.shadows is None:
+            return
+        r, members, views = 0, [], []
+        for n in pnames:
+            src = self.P[n]
+            ptr = src.data_ptr()
+            owner = SHADOW_OF.get(ptr)
+            if owner is not None and owner[1] != (id(self.shadows), key):
+                return  # shadowed elsewhere: this key is re-cast every step
+            views.append((ptr, t[r:r + src.shape[0]]))
+            members.append((n, ptr, src._version))
+            r += src.shape[0]
+        for ptr, v in views:
+            SHADOW_OF[ptr] = (v, (id(self.shadows), key))
+        self.shadows[key] = (t, members)
+
     def w(self, name):
         """weight `name.weight` in compute dtype"""
         key = name
         t = self._w.get(key)
         if t is None:
             src = self.P[name + ".weight"]
-            t = src if self.dt == torch.float32 else K.cast(src, self.dt)
+            if self.dt == torch.float32:
+                t = src
+            else:
+                t = self._shadow(key, [name + ".weight"])
+                if t is None:
+                    t = K.cast(src, self.dt)
+                    self._register(key, t, [name + ".weight"])
             self._w[key] = t
         return t
 
@@ -77,13 +134,18 @@ class StepCtx:
         key = "|".join(names)
         t = self._w.get(key)
         if t is None:
-            ws = [self.P[n + ".weight"] for n in names]
+            wn = [n + ".weight" for n in names]
+            ws = [self.P[n] for n in wn]
             rows = sum(w.shape[0] for w in ws)
-            t = torch.empty((rows, ws[0].shape[1]), device=ws[0].device, dtype=self.dt)
-            r = 0
-            for w in ws:
-                K.cast(w, self.dt, out=t[r:r + w.shape[0]])
-                r += w.shape[0]
+            t = self._shadow(key, wn) if self.dt != torch.float32 else None
+            if t is None:
+                t = torch.empty((rows, ws[0].shape[1]), device=ws[0].device, dtype=self.dt)
+                r = 0
+                for w in ws:
+                    K.cast(w, self.dt, out=t[r:r + w.shape[0]])
+                    r += w.shape[0]
+                if self.dt != torch.float32:
+                    self._register(key, t, wn)
             bs = [self.P[n + ".bias"] for n in names]
             bt = torch.empty(rows, device=ws[0].device, dtype=torch.float32)
             r = 0

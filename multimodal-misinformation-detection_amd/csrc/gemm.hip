@@ -763,9 +763,17 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
 
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
-                                     int64_t ldc, int64_t M, int64_t N, EpiArgs e) {
+                                     int64_t ldc, int64_t M, int64_t N, EpiArgs e, const float* __restrict__ rs_part,
+                                     float* __restrict__ rs_out, float rs_beta) {
   const uint32_t seed = (e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   const int64_t total = M * N;
+  if (rs_part) {  // the fused row sums' per-split partials (G8 split-K), summed in split order
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+      float t = 0.f;
+      for (int s = 0; s < splits; ++s) t += rs_part[(int64_t)s * M + m];
+      rs_out[m] = (rs_beta != 0.f ? rs_beta * rs_out[m] : 0.f) + t;
+    }
+  }
   if (e.vec && (N % 8) == 0) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total / 8; g += (int64_t)gridDim.x * blockDim.x) {
       float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1007,15 +1015,15 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   if (ws) {
     const int64_t total = a.M * a.N;
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-    if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc, a.M, a.N, e);
-    else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc, a.M, a.N, e);
+    // the row sums' split partials (rs_mode 2) are reduced by the same launch
+    const float* rsp = rs_mode == 2 ? rs_part : nullptr;
+    if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc,
+                                a.M, a.N, e, rsp, a.a_rowsum, a.a_rowsum_beta);
+    else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc,
+                            a.M, a.N, e, rsp, a.a_rowsum, a.a_rowsum_beta);
     MMFD_CHECK_LAUNCH("splitk_reduce");
   }
-  if (rs_mode == 2) {
-    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((a.M + 63) / 64)), dim3(1024), 0, s,
-                       (const float*)rs_part, splits, a.M, a.M, a.a_rowsum, a.a_rowsum_beta);
-    MMFD_CHECK_LAUNCH("gemm rowsum reduce");
-  } else if (a.a_rowsum && !g8) {
+  if (a.a_rowsum && !g8) {
     char* base = (char*)a.workspace + (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
     const int64_t left = a.workspace_bytes - (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
     return rowsum_fallback(a, base, left, s);

@@ -218,7 +218,7 @@ class _BertFn(torch.autograd.Function):
             raise NotImplementedError("mmfd BERT uses one dropout probability for hidden and attention dropout")
         dev = params[0].device
         sc = Bk.StepCtx(P, model.compute_dtype, p, model._fork_seed(dev) if training and p > 0 else None,
-                        training=training)
+                        training=training, shadows=Bk.shadow_store(model))
         sc.grad_ready = getattr(model, "_grad_ready", None)
         ids = input_ids.to(dev).long().contiguous()
         B, L = ids.shape
@@ -376,7 +376,7 @@ class _ViTFn(torch.autograd.Function):
         P = {n: p.detach() for n, p in zip(names, params)}
         P[PATCH_W] = P[PATCH_W].reshape(P[PATCH_W].shape[0], -1)  # conv16/s16 == GEMM over patches
         dev = params[0].device
-        sc = Bk.StepCtx(P, model.compute_dtype, 0.0, None, training=model.training)
+        sc = Bk.StepCtx(P, model.compute_dtype, 0.0, None, training=model.training, shadows=Bk.shadow_store(model))
         sc.grad_ready = getattr(model, "_grad_ready", None)
         out, st = vit_forward(sc, model.config, pixel_values.to(dev).float().contiguous(), keep)
         fctx.keep = keep
@@ -497,7 +497,7 @@ class MPNetModel(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("mmfd MPNetModel runs on the HIP device: call .to('cuda') first")
         P = {n: p.detach() for n, p in params.items()}
-        sc = Bk.StepCtx(P, self.compute_dtype)
+        sc = Bk.StepCtx(P, self.compute_dtype, shadows=Bk.shadow_store(self))
         ids = input_ids.to(dev).long().contiguous()
         mask = attention_mask.to(dev).long().contiguous() if attention_mask is not None else None
         out = mpnet_forward(sc, self.config, ids, mask, self._bucket(ids.shape[1], dev))

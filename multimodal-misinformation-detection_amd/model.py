@@ -114,7 +114,7 @@ class _HeadFn(torch.autograd.Function):
         names = model._param_names
         P = {n: p.detach() for n, p in zip(names, params)}
         sc = Bk.StepCtx(P, model.compute_dtype, model.dropout_p, model._get_seed() if model.training else None,
-                        training=model.training)
+                        training=model.training, shadows=Bk.shadow_store(model))
         sc.grad_ready = getattr(model, "_grad_ready", None)
         outs, state = FU.head_forward(sc, model._cfg, X_t, X_i, E_t, E_i)
         ctx.sc, ctx.state, ctx.model = sc, state, model

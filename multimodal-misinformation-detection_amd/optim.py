@@ -22,15 +22,21 @@ class AdamW(torch.optim.Optimizer):
         self._tables = {}
 
     def _table(self, entries, device):
-        key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s.data_ptr(), p.numel())
-                    for p, g, m, v, s in entries)
+        from .blocks import SHADOW_OF
+        shadows = []
+        for p, *_ in entries:  # the bf16 weight copies the HIP modules read (refreshed in the same launch)
+            sh = SHADOW_OF.get(p.data_ptr())
+            ok = sh is not None and sh[0].dtype == torch.bfloat16 and sh[0].numel() == p.numel()
+            shadows.append(sh[0].data_ptr() if ok else 0)
+        key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s.data_ptr(), p.numel(), sp)
+                    for (p, g, m, v, s), sp in zip(entries, shadows))
         t = self._tables.get(key)
         if t is None:
             arr = (K.AdamWTensor * len(entries))()
-            for i, (p, g, m, v, s) in enumerate(entries):
+            for i, ((p, g, m, v, s), sp) in enumerate(zip(entries, shadows)):
                 arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
                 arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
-                arr[i].param_bf16 = None
+                arr[i].param_bf16 = sp or None
                 arr[i].step = s.data_ptr()
                 arr[i].numel = p.numel()
             host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)

@@ -72,3 +72,41 @@ def test_config2_full_size_forward_logits(precision, tol):
         assert g.shape == w.shape
         err = (g.float().cpu() - w).abs().max().item()
         assert err < tol, (precision, err)
+
+
+def test_bf16_weight_shadows_follow_adamw_and_external_updates():
+    """bf16 steps read persistent bf16 copies of the master weights that mmfd AdamW refreshes in
+    its own launch: after several steps every registered copy equals bf16(master) exactly, and an
+    in-place update made outside AdamW (version bump) forces a re-cast on the next forward."""
+    from mmfd import blocks as Bk
+    from mmfd import kernels as K
+    tr, _ = build_pair("bf16", dropout=0.1)
+    for s in range(3):
+        tr.step({k: v.cuda() for k, v in tiny_batch(2, seed=30 + s).items()})
+    torch.cuda.synchronize()
+    named = {}
+    for m in (tr.text_encoder, tr.image_encoder, tr.head):
+        named.update({p.data_ptr(): p for p in m.parameters()})
+    checked = 0
+    for m in (tr.text_encoder, tr.image_encoder, tr.head):
+        for key, (t, members) in Bk.shadow_store(m).items():
+            r = 0
+            for n, ptr, ver in members:
+                p = named[ptr]
+                rows = p.shape[0]
+                assert torch.equal(t[r:r + rows].reshape(-1), K.cast(p.detach().reshape(-1), torch.bfloat16)), key
+                r += rows
+                checked += 1
+    assert checked > 20
+    # an external in-place update invalidates the copy
+    w = tr.head.classifier.mlp_text_given_text[0].weight if hasattr(tr.head, "classifier") else None
+    p = next(iter(tr.text_encoder.parameters())) if w is None else w
+    with torch.no_grad():
+        p.mul_(2.0)
+    store = Bk.shadow_store(tr.text_encoder if w is None else tr.head)
+    stale = [k for k, (t, mem) in store.items() if any(ptr == p.data_ptr() for _, ptr, _ in mem)]
+    for k in stale:
+        sc = Bk.StepCtx({n: q.detach() for n, q in (tr.text_encoder if w is None else tr.head).named_parameters()},
+                        torch.bfloat16, shadows=store)
+        names = [n for n, _, _ in store[k][1]]
+        assert sc._shadow(k, names) is None
