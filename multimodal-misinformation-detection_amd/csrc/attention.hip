@@ -584,13 +584,13 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float rs = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(s[ks][r] - mnew);
+          const float e = __builtin_amdgcn_exp2f(s[ks][r] - mnew);
           rs += e;
           float pe = e;
           if (p.p > 0.f) {
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
           const int lq = qs * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kb2);
           if (p.rel_bias && lq < p.Lq && mykey < p.Lk) t = fmaf(p.rel_bias[(h * p.Lq + lq) * p.Lk + mykey], LOG2E, t);
-          const float pr = exp2f(t - lq2[r]);
+          const float pr = __builtin_amdgcn_exp2f(t - lq2[r]);
           float z = 1.f;
           if (p.p > 0.f) {
             const uint32_t hsh = mmfd_hash_k(hkey, hcol + (uint64_t)lq * (uint64_t)p.Lk);
@@ -797,7 +797,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
           const int key = ks * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kbr[r]);
           if (relrow && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
-          const float pr = exp2f(t - lse2);
+          const float pr = __builtin_amdgcn_exp2f(t - lse2);
           float z = 1.f;
           if (p.p > 0.f) {
             const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)key);

@@ -49,15 +49,18 @@ template <> struct elem_traits<bf16>  { static constexpr int per16 = 8; static c
 // ---------------------------------------------------------------------------------------------
 // activations (exact erf GELU as nn.GELU() / HF "gelu")
 // ---------------------------------------------------------------------------------------------
-// erf(z) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), branch-free: one rcp, one exp2, five
-// FMAs (the libm erff is ~35 instructions with a divergent branch). e = exp(-z*z) is returned
-// too: GELU's derivative needs exp(-x*x/2) = exp(-z*z) for z = x/sqrt(2).
+// erf(z) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), branch-free: one v_rcp_f32, one
+// v_exp_f32 and five FMAs (the libm erff is ~35 instructions with a divergent branch; the
+// correctly rounded __frcp_rn / denormal-safe exp2f sequences cost ~10 more each). The hardware
+// rcp (1 ulp) and exp2 (flushes results below 2^-126, where the erf tail is exactly 1 in fp32)
+// stay inside the A&S bound. e = exp(-z*z) is returned too: GELU's derivative needs
+// exp(-x*x/2) = exp(-z*z) for z = x/sqrt(2).
 __device__ __forceinline__ float erf_fast(float z, float& e) {
   const float a = fabsf(z);
-  const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
   const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
                               0.254829592f);
-  e = exp2f(-a * a * 1.4426950408889634f);
+  e = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
   return copysignf(fmaf(-poly, e, 1.0f), z);
 }
 __device__ __forceinline__ float gelu_f(float x) {

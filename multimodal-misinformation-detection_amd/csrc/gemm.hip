@@ -13,6 +13,7 @@
 // The three nn.Linear products are (TA,TB) = (0,0) forward, (0,1) grad-input, (1,1) grad-weight.
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 #include <stdlib.h>
 
 namespace {
@@ -486,6 +487,21 @@ __device__ __forceinline__ float g8_rowsum(const char* img, int wr, int wc, int 
          g8_sum8(load_frag<bf16, LAYOUT, 128>(img, wr * 4 + wc, 1, lane));
 }
 
+// Diagnostic build only (-DMMFD_G8_STAMPS, tools/g8_stamps.py): per-wave s_memtime stamps at
+// the phase boundaries of the 256x256 kernel, to a buffer no computation reads.
+#ifdef MMFD_G8_STAMPS
+constexpr int G8_NSTAMP = 8;
+__device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
+#define G8_STAMP(k)                                                                                    \
+  do {                                                                                                 \
+    const uint64_t t__ = __builtin_amdgcn_s_memtime();                                                \
+    const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                                 \
+    if (lane == 0 && b__ < 16384) g8_stamps[(b__ * 8 + wave) * G8_NSTAMP + (k)] = t__;                \
+  } while (0)
+#else
+#define G8_STAMP(k) do { } while (0)
+#endif
+
 template <int TA, int TB, typename TC>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
@@ -496,6 +512,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  G8_STAMP(0);
   const int gx = gridDim.x, gy = gridDim.y;
   const int tile = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   const int64_t m0 = (int64_t)(tile / gx) * G8_BM, n0 = (int64_t)(tile % gx) * G8_BN;
@@ -590,9 +607,11 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     g8_mma(acc[1][0], fa, fb);
     g8_barrier();
   }
+  G8_STAMP(1);
   if (wr == 0) g8_barrier();  // re-align the wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  G8_STAMP(2);
   if (do_rs) {
     rs0 += __shfl_xor(rs0, 16, 64);
     rs0 += __shfl_xor(rs0, 32, 64);
@@ -636,8 +655,10 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     for (int u = 0; u < 8; ++u) bia[u] = e.bias ? e.bias[col + u] : 0.f;
     const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
     const bool fwd_act = e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU;
-#pragma unroll
-    for (int mq = 0; mq < 2; ++mq) {
+    // one pass per 128-row half; a lambda per pass (not an unrolled loop, whose body is too big to
+    // unroll) keeps every accumulator index a compile-time constant
+    auto pass = [&](auto mqc) {
+      constexpr int mq = decltype(mqc)::value;
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
@@ -646,73 +667,102 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
           for (int j = 0; j < 2; ++j)
             *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
                 acc[mq][nq][i][j];
+      if (mq == 0) G8_STAMP(3);
       __syncthreads();
+      if (mq == 0) G8_STAMP(4);
       constexpr int IT = 128 * (G8_BN / 8) / NT;  // 8 rows per thread, in two groups of 4
+      // every thread owns 8 columns of rows lr0 + 16 k (k < IT): the operand / output row pointers
+      // advance by a scalar stride (no per-row 64-bit address math), every epilogue branch is
+      // uniform, and the residual / aux / C loads of GI rows are in flight before their math
+      const int lr0 = tid / (G8_BN / 8);
+      const int64_t rstep = NT / (G8_BN / 8);  // 16 rows between a thread's rows
+      const int64_t rbase = m0 + mq * 128;     // uniform part of the row
+      // uniform (scalar) tile bases + 32-bit per-lane offsets (host-checked: operands < 2^31 elements)
+      const int oc = lr0 * (int)ldc + c8, orr = lr0 * (int)e.ldr + c8, oa = lr0 * (int)e.ldaux + c8;
+      TC* cp = C + rbase * ldc + n0 + oc;
+      const TC* rp = e.residual ? reinterpret_cast<const TC*>(e.residual) + rbase * e.ldr + n0 + orr : nullptr;
+      const TC* xp = bwd_act ? reinterpret_cast<const TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+      TC* ap = (fwd_act && e.aux) ? reinterpret_cast<TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+      const uint64_t hidx = (uint64_t)(rbase + lr0) * (uint64_t)N + (uint64_t)col;
+      const int64_t cs = rstep * ldc, rs = rstep * e.ldr, xs = rstep * e.ldaux;
+      const float* src = ct + lr0 * LDC + c8;
       constexpr int GI = 2;
 #pragma unroll
       for (int k0 = 0; k0 < IT; k0 += GI) {
-      Raw8<TC> rres[GI], raux[GI], rc[GI];
+        Raw8<TC> rres[GI], raux[GI], rc[GI];
 #pragma unroll
-      for (int k = 0; k < GI; ++k) {
-        const int64_t row = m0 + mq * 128 + tid / (G8_BN / 8) + (k0 + k) * (NT / (G8_BN / 8));
-        if (e.residual) rres[k].load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col);
-        if (bwd_act) raux[k].load(reinterpret_cast<const TC*>(e.aux) + row * e.ldaux + col);
-        if (e.beta != 0.f) rc[k].load(C + row * ldc + col);
-      }
-#pragma unroll
-      for (int k = 0; k < GI; ++k) {
-        const int lr = tid / (G8_BN / 8) + (k0 + k) * (NT / (G8_BN / 8));
-        const int64_t row = m0 + mq * 128 + lr;
-        const float* src = ct + lr * LDC + c8;
-        const float4 a4 = *reinterpret_cast<const float4*>(src), b4 = *reinterpret_cast<const float4*>(src + 4);
-        float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
-        float t[8];
-        if (e.residual && e.res_first) {
-          rres[k].get(t);
-#pragma unroll
-          for (int u = 0; u < 8; ++u) z[u] += t[u];
+        for (int k = 0; k < GI; ++k) {
+          const int kk = k0 + k;
+          if (rp) rres[k].load(rp + kk * rs);
+          if (xp) raux[k].load(xp + kk * xs);
+          if (e.beta != 0.f) rc[k].load(cp + kk * cs);
         }
-        if (fwd_act) {
-          if (e.aux) V8<TC>::store(reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col, z);
-          if (e.act == MMFD_ACT_GELU) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
-          } else {
+        for (int k = 0; k < GI; ++k) {
+          const int kk = k0 + k;
+          const float4 a4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC);
+          const float4 b4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC + 4);
+          float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-            for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+          for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
+          float t[8];
+          if (rp && e.res_first) {
+            rres[k].get(t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
           }
-        } else if (bwd_act) {
-          raux[k].get(t);
-          if (e.act == MMFD_ACT_GELU_BWD) {
+          if (fwd_act) {
+            if (ap) V8<TC>::store(ap + kk * xs, z);
+            if (e.act == MMFD_ACT_GELU) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
-          } else {
+              for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
+            } else {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+              for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+            }
+          } else if (xp) {
+            raux[k].get(t);
+            if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+            }
           }
-        }
-        if (e.p > 0.f) {
-          const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)col;
+          if (e.p > 0.f) {
+            const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
-        }
-        if (e.residual && !e.res_first) {
-          rres[k].get(t);
+            for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
+          }
+          if (rp && !e.res_first) {
+            rres[k].get(t);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) z[u] += t[u];
-        }
-        if (e.beta != 0.f) {
-          rc[k].get(t);
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (e.beta != 0.f) {
+            rc[k].get(t);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+            for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+          }
+          if (alpha == 23456.0f) {  // EXPERIMENT: everything but the global stores
+#pragma unroll
+            for (int u = 0; u < 8; ++u) asm volatile("" ::"v"(z[u]));
+            continue;
+          }
+          V8<TC>::store(cp + kk * cs, z);
         }
-        V8<TC>::store(C + row * ldc + col, z);
-      }
       }
       __syncthreads();
-    }
+      if (mq == 0) G8_STAMP(5);
+    };
+    pass(std::integral_constant<int, 0>{});
+    pass(std::integral_constant<int, 1>{});
+    G8_STAMP(6);
+#ifdef MMFD_G8_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    G8_STAMP(7);
+#endif
     return;
   }
 #pragma unroll
@@ -933,6 +983,12 @@ int rowsum_fallback(const mmfd_gemm_args& a, void* ws, int64_t ws_bytes, hipStre
 }
 
 }  // namespace
+
+#ifdef MMFD_G8_STAMPS
+extern "C" int mmfd_debug_g8_stamps(void* host_dst, int64_t bytes) {
+  return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g8_stamps), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
   if (!a) return 0;

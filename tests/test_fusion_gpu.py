@@ -92,13 +92,14 @@ def test_train_step_matches_reference_train_epoch():
         else:
             assert P[k].grad is None, k
     opt.step()
-    # AdamW's first step moves each element by ~lr * g / (|g| + eps): elements whose reference gradient
-    # is within fp32 noise of 0 (|g| < 1e-6) may legitimately move by up to lr; all others must agree
+    # AdamW's first step moves each element by ~lr * g / (|g| + eps): an element whose reference
+    # gradient is within fp32 noise of 0 (|g| < 1e-6) moves by up to lr in the direction of that
+    # noise's sign, so the two steps may differ by up to 2 lr there; all others must agree
     for k in names:
         post = P[k].detach().double().cpu()
         ref = torch.from_numpy(z["post/" + k]).double()
         diff = (post - ref).abs()
-        assert diff.max().item() <= 1.0001e-4 + 1e-6, k
+        assert diff.max().item() <= 2.0001e-4 + 1e-6, k
         if "grad/" + k in z.files:
             solid = torch.from_numpy(z["grad/" + k]).abs() > 1e-6
             worst = diff[solid].max().item() if solid.any() else 0.0

@@ -1,0 +1,55 @@
+"""Diagnostic: per-wave phase times of the 256x256 GEMM from s_memtime stamps (a separate
+-DMMFD_G8_STAMPS build of libmmfd_hip under tools/_stamps/; the product library is untouched).
+Stamps: 0 start, 1 mainloop done, 2 after the re-align + vmcnt(0) + barrier, 3 staging written,
+4 after the staging barrier, 5 first 128 rows read back + stored, 6 epilogue issued, 7 stores
+retired (vmcnt(0)).   python tools/g8_stamps.py [M N K]"""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+SRC = os.path.join(ROOT, "multimodal-misinformation-detection_amd", "csrc")
+LIB = os.path.join(ROOT, "tools", "_stamps", "libmmfd_hip_stamps.so")
+if not os.path.exists(LIB):
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    objs = []
+    for f in sorted(os.listdir(SRC)):
+        if f.endswith(".hip"):
+            o = os.path.join(os.path.dirname(LIB), f + ".o")
+            subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950",
+                            "-DMMFD_G8_STAMPS", "-c", os.path.join(SRC, f), "-o", o], check=True)
+            objs.append(o)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", LIB] + objs, check=True)
+
+import mmfd  # noqa: E402,F401
+from mmfd import kernels as K  # noqa: E402
+
+K.load(LIB)
+lib = K.lib()
+lib.mmfd_debug_g8_stamps.restype = ctypes.c_int
+lib.mmfd_debug_g8_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+M, N, Kd = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (65536, 3072, 768)
+A = torch.randn(M, Kd, device="cuda").bfloat16()
+B = torch.randn(N, Kd, device="cuda").bfloat16()
+out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+for _ in range(5):
+    K.gemm(A, B, out=out)
+torch.cuda.synchronize()
+nblk = min((M // 256) * (N // 256), 16384)
+buf = np.zeros(16384 * 8 * 8, np.uint64)
+assert lib.mmfd_debug_g8_stamps(buf.ctypes.data, buf.nbytes) == 0
+st = buf.reshape(16384, 8, 8)[:nblk].astype(np.int64)
+d = np.diff(st, axis=2)  # [blocks, waves, 7]
+names = ["mainloop", "realign+vmcnt+barrier", "stage writes", "stage barrier", "rows 0-127 epilogue",
+         "rows 128-255 epilogue", "store drain"]
+print(f"M={M} N={N} K={Kd}: {nblk} blocks; cycles per phase (median / p90 over waves)")
+for i, n in enumerate(names):
+    v = d[:, :, i].ravel()
+    print(f"  {n:24s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
+tot = st[:, :, 7] - st[:, :, 0]
+print(f"  {'total':24s} {np.median(tot):9.0f} {np.percentile(tot, 90):9.0f}")
