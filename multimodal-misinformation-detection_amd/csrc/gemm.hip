@@ -502,7 +502,9 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 #define G8_STAMP(k) do { } while (0)
 #endif
 
-template <int TA, int TB, typename TC>
+// PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
+// prefetched for all of a thread's rows before the accumulators are staged (see the epilogue)
+template <int TA, int TB, typename TC, bool PRE>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
@@ -659,6 +661,84 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     // unroll) keeps every accumulator index a compile-time constant
     auto pass = [&](auto mqc) {
       constexpr int mq = decltype(mqc)::value;
+      if constexpr (PRE) {
+        // exactly one operand stream (residual OR aux OR C; chosen on the host): all IT rows of it
+        // are loaded before the accumulators are staged, so their HBM latency overlaps the
+        // staging and its barrier instead of being paid once per row group
+        constexpr int IT = 128 * (G8_BN / 8) / NT;
+        const int lr0 = tid / (G8_BN / 8);
+        const int64_t rstep = NT / (G8_BN / 8);
+        const int64_t rbase = m0 + mq * 128;
+        const int oc = lr0 * (int)ldc + c8, orr = lr0 * (int)e.ldr + c8, oa = lr0 * (int)e.ldaux + c8;
+        TC* cp = C + rbase * ldc + n0 + oc;
+        const int64_t cs = rstep * ldc, rs = rstep * e.ldr, xs = rstep * e.ldaux;
+        const bool res = e.residual != nullptr;
+        const TC* lp = res ? reinterpret_cast<const TC*>(e.residual) + rbase * e.ldr + n0 + orr
+                           : bwd_act ? reinterpret_cast<const TC*>(e.aux) + rbase * e.ldaux + n0 + oa : cp;
+        const int64_t ls = res ? rs : (bwd_act ? xs : cs);
+        Raw8<TC> pre[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) pre[k].load(lp + k * ls);
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+                  acc[mq][nq][i][j];
+        __syncthreads();
+        TC* ap = (fwd_act && e.aux) ? reinterpret_cast<TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+        const uint64_t hidx = (uint64_t)(rbase + lr0) * (uint64_t)N + (uint64_t)col;
+        const float* src = ct + lr0 * LDC + c8;
+#pragma unroll
+        for (int kk = 0; kk < IT; ++kk) {
+          const float4 a4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC);
+          const float4 b4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC + 4);
+          float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
+          float t[8];
+          pre[kk].get(t);
+          if (res && e.res_first) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (fwd_act) {
+            if (ap) V8<TC>::store(ap + kk * xs, z);
+            if (e.act == MMFD_ACT_GELU) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+            }
+          } else if (bwd_act) {
+            if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+            }
+          }
+          if (e.p > 0.f) {
+            const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
+          }
+          if (res && !e.res_first) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (!res && !bwd_act) {  // the stream is C: beta * C
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+          }
+          V8<TC>::store(cp + kk * cs, z);
+        }
+        __syncthreads();
+      } else {
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
@@ -755,6 +835,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
       }
       __syncthreads();
       if (mq == 0) G8_STAMP(5);
+      }
     };
     pass(std::integral_constant<int, 0>{});
     pass(std::integral_constant<int, 1>{});
@@ -878,18 +959,29 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
                      a.alpha, tps, e);
 }
 
-template <int TA, int TB, typename TC>
-void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
-               int rs_mode, hipStream_t s) {
+template <int TA, int TB, typename TC, bool PRE>
+void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
+                 int rs_mode, hipStream_t s) {
   dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<TA, TB, TC>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<TA, TB, TC, PRE>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm256_kernel<TA, TB, TC>), grid, dim3(NT), G8_LDS, s, (const bf16*)a.A, a.lda,
+  hipLaunchKernelGGL((gemm256_kernel<TA, TB, TC, PRE>), grid, dim3(NT), G8_LDS, s, (const bf16*)a.A, a.lda,
                      (const bf16*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
                      a.a_rowsum_beta, rs_mode);
+}
+
+template <int TA, int TB, typename TC>
+void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
+               int rs_mode, hipStream_t s) {
+  const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
+  const int streams = (e.residual ? 1 : 0) + (bwd_act ? 1 : 0) + (e.beta != 0.f ? 1 : 0);
+  if constexpr (std::is_same<TC, bf16>::value) {
+    if (streams == 1 && !ws && e.vec) return launch_g8_v<TA, TB, TC, true>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  }
+  launch_g8_v<TA, TB, TC, false>(a, e, ws, splits, tps, rs_out, rs_mode, s);
 }
 
 template <typename TC>

@@ -14,7 +14,7 @@ import zlib
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmmfd_hip.so")
+LIB_PATH = os.environ.get("MMFD_LIB_PATH") or os.path.join(_HERE, "libmmfd_hip.so")  # env override: A/B runs of two builds (tools/ab.sh)
 
 F32, BF16, F16 = 0, 1, 2
 COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4

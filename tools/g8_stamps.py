@@ -2,7 +2,7 @@
 -DMMFD_G8_STAMPS build of libmmfd_hip under tools/_stamps/; the product library is untouched).
 Stamps: 0 start, 1 mainloop done, 2 after the re-align + vmcnt(0) + barrier, 3 staging written,
 4 after the staging barrier, 5 first 128 rows read back + stored, 6 epilogue issued, 7 stores
-retired (vmcnt(0)).   python tools/g8_stamps.py [M N K]"""
+retired (vmcnt(0)).   python tools/g8_stamps.py [M N K [plain|gelu|gelubwd]]"""
 import ctypes
 import os
 import subprocess
@@ -37,8 +37,16 @@ M, N, Kd = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (65536, 307
 A = torch.randn(M, Kd, device="cuda").bfloat16()
 B = torch.randn(N, Kd, device="cuda").bfloat16()
 out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+kind = sys.argv[4] if len(sys.argv) > 4 else "plain"
+aux = torch.randn(M, N, device="cuda").bfloat16()
+bias = torch.randn(N, device="cuda")
 for _ in range(5):
-    K.gemm(A, B, out=out)
+    if kind == "gelu":
+        K.gemm(A, B, out=out, bias=bias, act=K.ACT_GELU, aux=aux)
+    elif kind == "gelubwd":
+        K.gemm(A, B, out=out, act=K.ACT_GELU_BWD, aux=aux)
+    else:
+        K.gemm(A, B, out=out)
 torch.cuda.synchronize()
 nblk = min((M // 256) * (N // 256), 16384)
 buf = np.zeros(16384 * 8 * 8, np.uint64)
@@ -47,7 +55,7 @@ st = buf.reshape(16384, 8, 8)[:nblk].astype(np.int64)
 d = np.diff(st, axis=2)  # [blocks, waves, 7]
 names = ["mainloop", "realign+vmcnt+barrier", "stage writes", "stage barrier", "rows 0-127 epilogue",
          "rows 128-255 epilogue", "store drain"]
-print(f"M={M} N={N} K={Kd}: {nblk} blocks; cycles per phase (median / p90 over waves)")
+print(f"M={M} N={N} K={Kd} {kind}: {nblk} blocks; cycles per phase (median / p90 over waves)")
 for i, n in enumerate(names):
     v = d[:, :, i].ravel()
     print(f"  {n:24s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
