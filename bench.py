@@ -4,7 +4,7 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency]
 """
 import argparse
 import json
@@ -324,6 +324,67 @@ def preprocess_main(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def latency_main(args, dev, world, rank):
+    """single-pair inference of evaluate.py:95-192 (claim + evidence text padded
+    to max_length 512, two 224x224 images, bert-base-uncased + ViT-B/16 + fusion head, eval) through
+    mmfd.predict.MisinformationPredictor; a step = one pair, inputs already resident in HBM. The
+    HIP-graph replay is the value; the eager (per-kernel Python launch) latency is reported beside
+    it. Each rank runs its own replica (no collective)."""
+    from mmfd.predict import MisinformationPredictor
+    from mmfd.train import build_flagship
+
+    tr = build_flagship(dev, args.precision, seed=42 + rank)
+    g = torch.Generator(device="cpu").manual_seed(77 + rank)
+    L = 512
+
+    def pair():
+        ids = torch.randint(1000, 30522, (L,), generator=g)
+        ids[0], ids[-1] = 101, 102
+        return ids.to(dev), torch.ones(L, dtype=torch.long, device=dev), torch.randn(3, 224, 224, generator=g).to(dev)
+
+    c, e = pair(), pair()
+    res = {}
+    for mode in ("eager", "graph"):
+        pr = MisinformationPredictor.from_trainer(tr, use_graph=mode == "graph")
+        for _ in range(max(1, args.warmup)):
+            pr.predict_logits(*c, *e)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pr.predict_logits(*c, *e)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        res[mode] = t.item() / args.steps * 1e3
+    if rank == 0:
+        # algorithmic forward FLOPs of the pair at L=512 (FlopCounterMode-style matmul count):
+        # BERT 2 x (12 x (4 x 512 x 768^2 x 2 + 2 x 512 x 768 x 3072 x 2 + 2 x 512^2 x 768 x 2)),
+        # ViT 2 x 35.126 GFLOP, fusion head 2.266 GFLOP (SURVEY 8(a))
+        bert = 12 * (4 * 512 * 768 * 768 * 2 + 2 * 512 * 768 * 3072 * 2 + 2 * 512 * 512 * 768 * 2)
+        flops = 2 * bert + 2 * 35.126e9 + 2.266e9
+        out = {"metric": "single claim-evidence pair latency (evaluate.py path, L=512)",
+               "value": round(res["graph"], 3), "unit": "ms/pair", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(res["graph"], 3), "higher_is_better": False,
+               "scaling": "replicas", "vs_baseline": None, "dtype": args.precision,
+               "data": "synthetic pair (512-token texts, 224x224 images, random-init weights)",
+               "config": {"workload": "single-pair inference (SURVEY 8f row 4): bert-base-uncased + ViT-B/16 + "
+                                      "fusion head, HIP graph replay", "global_batch": 1, "seq_len": L,
+                          "image_size": 224, "parallelism": f"replicas{world}"},
+               "eager_ms_per_pair": round(res["eager"], 3),
+               "tflops_graph": round(flops / (res["graph"] * 1e-3) / 1e12, 1)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -333,7 +394,8 @@ def main():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess"], default="train")
+    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess", "latency"],
+                    default="train")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -361,6 +423,8 @@ def main():
         return forward_main(args, dev, world, rank)
     if args.workload == "preprocess":
         return preprocess_main(args, dev, world, rank)
+    if args.workload == "latency":
+        return latency_main(args, dev, world, rank)
     tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 

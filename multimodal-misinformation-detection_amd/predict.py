@@ -1,0 +1,121 @@
+"""Single-pair inference: `MisinformationPredictor.evaluate` of the reference's
+evaluate.py:12-196 (and the per-pair voting input of app.py:313-371) on the HIP path.
+
+Reference flow (evaluate.py:95-192): tokenize claim and evidence to max_length=512 with padding,
+run the text encoder on each, the image encoder on each preprocessed image, the fusion model on
+(X_t, X_i, E_t, E_i), then per path softmax -> argmax -> label ("support" /
+"not_enough_information" / "refute", :82). Here:
+
+  * claim and evidence go through each encoder as ONE stacked batch of 2 (same weights);
+  * the whole forward (encoders + fusion head, eval mode) is captured once into a HIP graph on
+    static input buffers and replayed per pair, so a pair costs one graph launch instead of ~400
+    kernel launches from Python (`use_graph=False` runs the same kernels eagerly);
+  * inputs are token ids / attention masks (no tokenizer vocabulary ships offline) and normalised
+    pixel tensors; `mmfd.preprocess.ImagePreprocessor` produces the latter from decoded images.
+"""
+from __future__ import annotations
+
+import torch
+
+from .train import FusionTrainer
+
+IDX_TO_LABEL = {0: "support", 1: "not_enough_information", 2: "refute"}  # evaluate.py:82
+PATHS = ("text_text", "text_image", "image_text", "image_image")
+
+
+class MisinformationPredictor:
+    """Drop-in for evaluate.py:12 on already-built HIP modules (text encoder, image encoder,
+    `mmfd.model.MisinformationDetectionModel`), all on one device."""
+
+    def __init__(self, text_encoder, image_encoder, model, max_length=512, image_size=224, use_graph=True,
+                 device=None):
+        self.text_encoder, self.image_encoder, self.model = text_encoder, image_encoder, model
+        for m in (text_encoder, image_encoder, model):
+            m.eval()
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        if self.device.type != "cuda":
+            raise RuntimeError("MisinformationPredictor runs on the HIP device")
+        self.max_length, self.image_size = max_length, image_size
+        self.use_graph = use_graph
+        self.idx_to_label = dict(IDX_TO_LABEL)
+        self._graph = None
+        L, S = max_length, image_size
+        # static inputs of the captured forward: [claim, evidence] stacked
+        self._ids = torch.zeros(2, L, dtype=torch.int64, device=self.device)
+        self._mask = torch.zeros(2, L, dtype=torch.int64, device=self.device)
+        self._px = torch.zeros(2, 3, S, S, dtype=torch.float32, device=self.device)
+        self._out = None
+
+    @classmethod
+    def from_trainer(cls, trainer: FusionTrainer, **kw):
+        return cls(trainer.text_encoder, trainer.image_encoder, trainer.head, **kw)
+
+    @torch.no_grad()
+    def _forward(self):
+        T = self.text_encoder(input_ids=self._ids, attention_mask=self._mask).last_hidden_state
+        I = self.image_encoder(self._px).last_hidden_state
+        (ytt, yti), (yit, yii) = self.model(T[:1], I[:1], T[1:], I[1:])
+        return ytt, yti, yit, yii
+
+    def _capture(self):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up: one-time casts of the weight shadows, kernel attributes
+                self._forward()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._out = self._forward()
+        self._graph = g
+
+    def _load(self, claim_ids, claim_mask, claim_pixels, evidence_ids, evidence_mask, evidence_pixels):
+        L = self.max_length
+        for row, (ids, mask) in enumerate(((claim_ids, claim_mask), (evidence_ids, evidence_mask))):
+            ids = torch.as_tensor(ids).reshape(-1)[:L]  # truncation=True (evaluate.py:113-126)
+            mask = torch.ones_like(ids) if mask is None else torch.as_tensor(mask).reshape(-1)[:L]
+            self._ids[row].zero_()
+            self._mask[row].zero_()
+            self._ids[row, :ids.numel()].copy_(ids, non_blocking=True)  # padding="max_length"
+            self._mask[row, :mask.numel()].copy_(mask, non_blocking=True)
+        for row, px in enumerate((claim_pixels, evidence_pixels)):
+            px = torch.as_tensor(px)
+            if px.dim() == 4:
+                px = px[0]
+            if tuple(px.shape) != (3, self.image_size, self.image_size):
+                raise ValueError(f"pixel tensor must be [3, {self.image_size}, {self.image_size}], got {tuple(px.shape)}")
+            self._px[row].copy_(px, non_blocking=True)
+
+    @torch.no_grad()
+    def predict_logits(self, claim_ids, claim_mask, claim_pixels, evidence_ids, evidence_mask, evidence_pixels):
+        """((y_tt, y_ti), (y_it, y_ii)) logits [1, num_classes] for one pair (model.py:426-468)."""
+        self._load(claim_ids, claim_mask, claim_pixels, evidence_ids, evidence_mask, evidence_pixels)
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+            out = self._out
+        else:
+            out = self._forward()
+        ytt, yti, yit, yii = (o.clone() for o in out)
+        return (ytt, yti), (yit, yii)
+
+    def process_output(self, output):
+        """softmax -> argmax -> {label, confidence, probabilities} (evaluate.py:169-182)."""
+        if output is None:
+            return None
+        probs = torch.softmax(output.float(), dim=-1)[0].cpu()
+        idx = int(probs.argmax())
+        return {"label": self.idx_to_label[idx], "confidence": float(probs[idx]),
+                "probabilities": {self.idx_to_label[i]: float(p) for i, p in enumerate(probs)}}
+
+    def evaluate(self, claim_ids, claim_mask, claim_pixels, evidence_ids, evidence_mask, evidence_pixels,
+                 details=False):
+        """path -> label for the four modality paths (evaluate.py:184-192); `details` returns the
+        full process_output dicts instead of the labels."""
+        (ytt, yti), (yit, yii) = self.predict_logits(claim_ids, claim_mask, claim_pixels, evidence_ids,
+                                                     evidence_mask, evidence_pixels)
+        preds = {p: self.process_output(y) for p, y in zip(PATHS, (ytt, yti, yit, yii))}
+        if details:
+            return preds
+        return {p: (d["label"] if d else None) for p, d in preds.items()}
