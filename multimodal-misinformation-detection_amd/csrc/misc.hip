@@ -23,6 +23,48 @@ __global__ void seq_mean_fwd_kernel(int64_t B, int64_t L, int64_t D, const T* __
     out[b * ldo + d] = from_f32<T>(s / (float)L);
   }
 }
+__device__ __forceinline__ void load8(const bf16* p, float (&v)[8]) {
+  const uint4 w = *reinterpret_cast<const uint4*>(p);
+  const uint32_t a[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(a[i] << 16); v[2 * i + 1] = __uint_as_float(a[i] & 0xffff0000u); }
+}
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+// vector form (D % 8 == 0, 16-B aligned rows): block = 32 column chunks of 8 x 32 row groups;
+// each thread sums every 32nd row of its chunk with 16-B loads (all independent, so a short batch
+// with long sequences is not a serial chain of L dependent loads), then the 32 row-group partials
+// are combined in LDS in a fixed order.
+template <typename T>
+__global__ void __launch_bounds__(1024) seq_mean_fwd_vec_kernel(int64_t L, int64_t D, const T* __restrict__ x,
+                                                                T* __restrict__ out, int64_t ldo) {
+  __shared__ float part[32][32 * 8 + 4];
+  const int cc = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int64_t b = blockIdx.y, c8 = ((int64_t)blockIdx.x * 32 + cc) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 < D) {
+    const T* p = x + b * L * D + c8;
+    for (int64_t l = rg; l < L; l += 32) {
+      float v[8];
+      load8(p + l * D, v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += v[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) part[rg][cc * 8 + u] = acc[u];
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int col = threadIdx.x;  // 32 chunks x 8 columns
+    const int64_t d = (int64_t)blockIdx.x * 256 + col;
+    float t = 0.f;
+    for (int r = 0; r < 32; ++r) t += part[r][col];
+    if (d < D) out[b * ldo + d] = from_f32<T>(t / (float)L);
+  }
+}
+
 template <typename T>
 __global__ void seq_mean_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dout, int64_t ldo,
                                     T* __restrict__ dx) {
@@ -218,6 +260,30 @@ __global__ void patchify_kernel(int64_t B, int64_t C, int64_t Hh, int64_t Ww, in
     for (int64_t kw = 0; kw < P; ++kw) dst[kw] = from_f32<T>(src[kw]);
   }
 }
+// vector form (P % 4 == 0, Ww % 4 == 0, 16-B aligned pixels): one thread per 4 consecutive
+// source pixels of an image row (coalesced float4 loads), stored as 4 consecutive patch-row
+// elements (8-B bf16 / 16-B fp32 stores)
+template <typename T>
+__global__ void patchify_vec_kernel(int64_t B, int64_t C, int64_t Hh, int64_t Ww, int64_t P,
+                                    const float* __restrict__ px, T* __restrict__ out) {
+  const int64_t nph = Hh / P, npw = Ww / P, np = nph * npw, w4n = Ww / 4;
+  const int64_t total = B * C * nph * P * w4n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w4 = i % w4n, h = (i / w4n) % (nph * P), c = (i / (w4n * nph * P)) % C, b = i / (w4n * nph * P * C);
+    const int64_t w = w4 * 4, ph = h / P, kh = h % P, pw = w / P, kw = w % P;
+    const float4 v = *reinterpret_cast<const float4*>(px + ((b * C + c) * Hh + h) * Ww + w);
+    T* dst = out + (b * np + ph * npw + pw) * (C * P * P) + (c * P + kh) * P + kw;
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, from_f32<T>(v.x)) |
+                          ((uint32_t)__builtin_bit_cast(uint16_t, from_f32<T>(v.y)) << 16);
+      const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, from_f32<T>(v.z)) |
+                          ((uint32_t)__builtin_bit_cast(uint16_t, from_f32<T>(v.w)) << 16);
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+    } else {
+      *reinterpret_cast<float4*>(dst) = v;
+    }
+  }
+}
 template <typename T>
 __global__ void vit_tokens_fwd_kernel(int64_t B, int64_t NP, int64_t D, const T* __restrict__ patch,
                                       const float* __restrict__ cls, const float* __restrict__ pos, T* __restrict__ out) {
@@ -287,6 +353,16 @@ extern "C" int mmfd_seq_mean_fwd(int dtype, int64_t B, int64_t L, int64_t D, con
                                  mmfd_stream_t stream) {
   MMFD_CHECK_ARG(L > 0, "seq_mean: L must be > 0");
   hipStream_t s = (hipStream_t)stream;
+  const int esz = dtype == MMFD_BF16 ? 2 : 4;
+  if (D % 8 == 0 && ((uintptr_t)x % 16) == 0 && (D * esz) % 16 == 0) {
+    const dim3 grid((unsigned)((D + 255) / 256), (unsigned)B);
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((seq_mean_fwd_vec_kernel<bf16>), grid, dim3(1024), 0, s, L, D, (const bf16*)x, (bf16*)out, ldo);
+    else
+      hipLaunchKernelGGL((seq_mean_fwd_vec_kernel<float>), grid, dim3(1024), 0, s, L, D, (const float*)x, (float*)out, ldo);
+    MMFD_CHECK_LAUNCH("seq_mean_fwd");
+    return 0;
+  }
   if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((seq_mean_fwd_kernel<bf16>), dim3(gridn(B * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)x, (bf16*)out, ldo);
   else
@@ -403,6 +479,15 @@ extern "C" int mmfd_patchify(int dtype, int64_t B, int64_t C, int64_t Hh, int64_
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = B * (Hh / P) * (Ww / P) * C * P;
   if (total == 0) return 0;
+  if (P % 4 == 0 && Ww % 4 == 0 && ((uintptr_t)pixels % 16) == 0 && ((uintptr_t)out % 16) == 0) {
+    const int64_t vt = total * P / 4;
+    if (dtype == MMFD_BF16)
+      hipLaunchKernelGGL((patchify_vec_kernel<bf16>), dim3(gridn(vt, 256)), dim3(256), 0, s, B, C, Hh, Ww, P, pixels, (bf16*)out);
+    else
+      hipLaunchKernelGGL((patchify_vec_kernel<float>), dim3(gridn(vt, 256)), dim3(256), 0, s, B, C, Hh, Ww, P, pixels, (float*)out);
+    MMFD_CHECK_LAUNCH("patchify");
+    return 0;
+  }
   if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((patchify_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, C, Hh, Ww, P, pixels, (bf16*)out);
   else

@@ -261,8 +261,10 @@ class GemmProbe:
 def _kernel_name(a, split):
     """the device kernel mmfd_gemm launches for these arguments (rocprof's demangled name)"""
     t = {F32: "float", BF16: "__bf16"}
-    if a.dtype == BF16:  # 256x256 kernel (gemm.hip use_g8)
-        base = f"gemm256_kernel<{a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
+    if a.dtype == BF16:  # 256x256 kernel (gemm.hip use_g8); PRE = one prefetched epilogue operand stream
+        streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD)) + int(a.beta != 0.0)
+        pre = a.c_dtype == BF16 and streams == 1 and not split
+        base = f"gemm256_kernel<{a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, {'true' if pre else 'false'}>"
     else:
         base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")

@@ -291,6 +291,21 @@ def test_layernorm(dtype, width, eps):
     assert (db.double().cpu() - br.grad).abs().max().item() < 1e-3 * R ** 0.5
 
 
+@pytest.mark.parametrize("B,L,D,dt", [(1, 512, 256, torch.bfloat16), (3, 197, 200, torch.float32),
+                                       (2, 7, 520, torch.bfloat16), (2, 9, 12, torch.float32)])
+def test_seq_mean_shapes(B, L, D, dt):
+    """vector kernel (D % 8 == 0: one-block-per-row-of-chunks, partial last block) and the scalar
+    fallback (D = 12); output into a wider buffer (ldo > D) as the fusion head's concat does"""
+    x = _rand(B, L, D, seed=41).to(dt)
+    buf = torch.zeros(B, D + 8, device=DEV, dtype=dt)
+    K.seq_mean_fwd(x.to(DEV), out=buf[:, :D])
+    torch.cuda.synchronize()
+    ref = x.double().mean(1)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert (buf[:, :D].double().cpu() - ref).abs().max().item() < tol
+    assert (buf[:, D:] == 0).all()
+
+
 def test_seq_mean_xent():
     x = _rand(4, 13, 256, seed=40)
     m = K.seq_mean_fwd(x.to(DEV))
