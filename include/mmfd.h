@@ -102,7 +102,8 @@ int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, flo
 /* Multi-head attention (unmasked fusion-head MHA layers.py:36-58 incl. the SDPA branch 44-49;  */
 /* HF BERT/ViT/MPNet self-attention called at train.py:137-143).                              */
 /* Q/K/V/O are addressed per (batch b, token t, head h) as base + b*s_b + t*s_t + h*D.         */
-/*   S = scale * Q K^T (+ key_bias[b][k]) (+ rel_bias[h][q][k]);  P = softmax(S);              */
+/*   S = scale * Q K^T (+ key_bias[b][k]) (+ rel_bias[b*rel_bias_sb + (h*Lq+q)*Lk + k]);        */
+/*   P = softmax(S)                                                                           */
 /*   O = dropout(P) V ;   lse[b][h][q] = log sum_k exp(S) (fp32)                                */
 /* ------------------------------------------------------------------------------------------- */
 typedef struct mmfd_attn_args {
@@ -115,7 +116,8 @@ typedef struct mmfd_attn_args {
   void* o; int64_t o_sb, o_st;
   float* lse;                      /* [B][H][Lq] */
   const float* key_bias;           /* [B][Lk] additive (HF extended attention mask) or NULL */
-  const float* rel_bias;           /* [H][Lq][Lk] additive (MPNet relative position) or NULL */
+  const float* rel_bias;           /* [H][Lq][Lk] additive (MPNet relative position; rel_bias_sb = 0)
+                                      or [B][H][Lq][Lk] (DeBERTa c2p + p2c; rel_bias_sb = H*Lq*Lk) */
   float dropout_p; const uint64_t* seed; uint64_t salt;  /* index = ((b*H+h)*Lq+q)*Lk+k */
   /* backward only */
   const void* dout; int64_t do_sb, do_st;   /* same head layout as o */
@@ -126,6 +128,7 @@ typedef struct mmfd_attn_args {
   float* d_rel_bias;               /* must be NULL (the relative bias is inference-only, MPNet) */
   int accumulate_dq;               /* 1: dq += result (else overwrite) */
   int accumulate_dkv;              /* 1: dk += ..., dv += ... */
+  int64_t rel_bias_sb;             /* batch stride of rel_bias in floats (0 = shared by the batch) */
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);
@@ -191,6 +194,23 @@ int mmfd_position_ids(int64_t B, int64_t L, const int64_t* input_ids, int64_t pa
    bucket int32 [Lq][Lk] (host-computed with the reference's bucket formula), table fp32 [nb][H] */
 int mmfd_rel_bias(int64_t H, int64_t Lq, int64_t Lk, const int32_t* bucket, const float* table, float* out,
                   mmfd_stream_t stream);
+/* DeBERTa-v3 (the reference's default text encoder, train.py:330-331; transformers
+   modeling_deberta_v2.py). Disentangled bias for the attention's rel_bias ([B][H][L][L] fp32):
+   out[b][h][i][j] = c2p[h][b*L+i][c2p_idx[i][j]] * inv_scale + p2c[h][b*L+j][p2c_idx[j][i]] * inv_scale
+   with c2p = Q_h . posK_h^T and p2c = K_h . posQ_h^T ([H][B*L][ld], dtype), the clamped log-bucket
+   indices int32 [L][L] computed on the host (modeling_deberta_v2.py:276-346). */
+int mmfd_deberta_rel_bias(int dtype, int64_t B, int64_t H, int64_t L, const void* c2p, const void* p2c, int64_t ld,
+                          const int32_t* c2p_idx, const int32_t* p2c_idx, float inv_scale, float* out,
+                          mmfd_stream_t stream);
+/* x[r][:] = 0 where mask[r] == 0 (DebertaV2Embeddings: embeddings * mask, :552-559), x [rows][ldx] */
+int mmfd_mask_rows(int dtype, int64_t rows, int64_t D, void* x, int64_t ldx, const int64_t* mask,
+                   mmfd_stream_t stream);
+/* attention rows of fully masked queries (mask[b][i] == 0): masked_fill(finfo.min) + softmax gives
+   them uniform weights over ALL Lk keys (modeling_deberta_v2.py:252-256), i.e. o = mean_k v.
+   q-layout views as in mmfd_attn_args (v: base + b*v_sb + t*v_st + h*D). */
+int mmfd_attn_fill_masked_rows(int dtype, int64_t B, int64_t H, int64_t L, int64_t Dh, const void* v, int64_t v_sb,
+                               int64_t v_st, void* o, int64_t o_sb, int64_t o_st, const int64_t* mask,
+                               mmfd_stream_t stream);
 /* scatter-add the gradient of the pre-LN sum into the three tables (fp32 atomics for word). */
 int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
                    const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos,

@@ -543,3 +543,112 @@ extern "C" int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, flo
   MMFD_CHECK_LAUNCH("mask_to_bias");
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// DeBERTa-v3 helpers (transformers modeling_deberta_v2.py; the reference's default text encoder)
+// ---------------------------------------------------------------------------------------------
+namespace {
+// one thread per (b, h, i, j), j fastest (coalesced fp32 output rows); the c2p gather stays inside
+// row (b, i) of head h, the p2c gather walks rows (b, j)
+template <typename T>
+__global__ void deberta_rel_bias_kernel(int64_t B, int64_t H, int64_t L, const T* __restrict__ c2p,
+                                        const T* __restrict__ p2c, int64_t ld, const int32_t* __restrict__ c2p_idx,
+                                        const int32_t* __restrict__ p2c_idx, float inv_scale, float* __restrict__ out) {
+  const int64_t total = B * H * L * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = e % L, i = (e / L) % L, h = (e / (L * L)) % H, b = e / (L * L * H);
+    const int64_t hb = h * B * L + b * L;
+    const float c = to_f32(c2p[(hb + i) * ld + c2p_idx[i * L + j]]);
+    const float q = to_f32(p2c[(hb + j) * ld + p2c_idx[j * L + i]]);
+    out[e] = c * inv_scale + q * inv_scale;  // score += c2p / scale; score += p2c / scale (:329, :345)
+  }
+}
+
+template <typename T>
+__global__ void mask_rows_kernel(int64_t rows, int64_t D, T* __restrict__ x, int64_t ldx,
+                                 const int64_t* __restrict__ mask) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < rows * D; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / D, d = e % D;
+    if (mask[r] == 0) x[r * ldx + d] = from_f32<T>(0.f);
+  }
+}
+
+// one block per (b, h): blocks of a batch row without padding return at once; otherwise Dh threads
+// (x up to 4 row groups) average v over all L keys in fp32 and write the masked query rows
+template <typename T>
+__global__ void __launch_bounds__(256) attn_fill_masked_rows_kernel(int64_t H, int64_t L, int64_t Dh,
+                                                                    const T* __restrict__ v, int64_t v_sb, int64_t v_st,
+                                                                    T* __restrict__ o, int64_t o_sb, int64_t o_st,
+                                                                    const int64_t* __restrict__ mask) {
+  const int64_t b = blockIdx.x / H, h = blockIdx.x % H;
+  __shared__ int any;
+  __shared__ float part[4][64];
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < L; i += blockDim.x)
+    if (mask[b * L + i] == 0) any = 1;
+  __syncthreads();
+  if (!any) return;
+  const int d = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (d < Dh)
+    for (int64_t t = rg; t < L; t += 4) s += to_f32(v[b * v_sb + t * v_st + h * Dh + d]);
+  part[rg][d] = s;
+  __syncthreads();
+  if (rg == 0 && d < Dh) {
+    const T mean = from_f32<T>((part[0][d] + part[1][d] + part[2][d] + part[3][d]) / (float)L);
+    for (int64_t i = 0; i < L; ++i)
+      if (mask[b * L + i] == 0) o[b * o_sb + i * o_st + h * Dh + d] = mean;
+  }
+}
+}  // namespace
+
+extern "C" int mmfd_deberta_rel_bias(int dtype, int64_t B, int64_t H, int64_t L, const void* c2p, const void* p2c,
+                                     int64_t ld, const int32_t* c2p_idx, const int32_t* p2c_idx, float inv_scale,
+                                     float* out, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(B >= 0 && H > 0 && L >= 0 && ld > 0, "deberta_rel_bias: bad shape");
+  MMFD_CHECK_ARG(dtype == MMFD_F32 || dtype == MMFD_BF16, "deberta_rel_bias: bad dtype");
+  const int64_t total = B * H * L * L;
+  if (total == 0) return 0;
+  MMFD_CHECK_ARG(c2p && p2c && c2p_idx && p2c_idx && out, "deberta_rel_bias: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((deberta_rel_bias_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, H, L,
+                       (const bf16*)c2p, (const bf16*)p2c, ld, c2p_idx, p2c_idx, inv_scale, out);
+  else
+    hipLaunchKernelGGL((deberta_rel_bias_kernel<float>), dim3(gridn(total, 256)), dim3(256), 0, s, B, H, L,
+                       (const float*)c2p, (const float*)p2c, ld, c2p_idx, p2c_idx, inv_scale, out);
+  MMFD_CHECK_LAUNCH("deberta_rel_bias");
+  return 0;
+}
+
+extern "C" int mmfd_mask_rows(int dtype, int64_t rows, int64_t D, void* x, int64_t ldx, const int64_t* mask,
+                              mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(rows >= 0 && D >= 0 && ldx >= D, "mask_rows: bad shape");
+  if (rows * D == 0) return 0;
+  MMFD_CHECK_ARG(x && mask, "mask_rows: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((mask_rows_kernel<bf16>), dim3(gridn(rows * D, 256)), dim3(256), 0, s, rows, D, (bf16*)x, ldx, mask);
+  else
+    hipLaunchKernelGGL((mask_rows_kernel<float>), dim3(gridn(rows * D, 256)), dim3(256), 0, s, rows, D, (float*)x, ldx, mask);
+  MMFD_CHECK_LAUNCH("mask_rows");
+  return 0;
+}
+
+extern "C" int mmfd_attn_fill_masked_rows(int dtype, int64_t B, int64_t H, int64_t L, int64_t Dh, const void* v,
+                                          int64_t v_sb, int64_t v_st, void* o, int64_t o_sb, int64_t o_st,
+                                          const int64_t* mask, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(B >= 0 && H > 0 && L >= 0 && Dh > 0 && Dh <= 64, "attn_fill_masked_rows: bad shape (Dh <= 64)");
+  if (B * L == 0) return 0;
+  MMFD_CHECK_ARG(v && o && mask, "attn_fill_masked_rows: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((attn_fill_masked_rows_kernel<bf16>), dim3((unsigned)(B * H)), dim3(256), 0, s, H, L, Dh,
+                       (const bf16*)v, v_sb, v_st, (bf16*)o, o_sb, o_st, mask);
+  else
+    hipLaunchKernelGGL((attn_fill_masked_rows_kernel<float>), dim3((unsigned)(B * H)), dim3(256), 0, s, H, L, Dh,
+                       (const float*)v, v_sb, v_st, (float*)o, o_sb, o_st, mask);
+  MMFD_CHECK_LAUNCH("attn_fill_masked_rows");
+  return 0;
+}

@@ -75,6 +75,7 @@ class AttnArgs(ctypes.Structure):
         ("d_rel_bias", ctypes.c_void_p),
         ("accumulate_dq", ctypes.c_int),
         ("accumulate_dkv", ctypes.c_int),
+        ("rel_bias_sb", ctypes.c_int64),
     ]
 
 
@@ -117,6 +118,9 @@ SIGNATURES = {
     "mmfd_maxpool_nhwc": (_I, [_I, _I64, _I64, _I64, _I64, _I, _I, _I, _I64, _I64, _VP, _VP, _VP]),
     "mmfd_global_avgpool": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP]),
     "mmfd_rel_bias": (_I, [_I64, _I64, _I64, _VP, _VP, _VP, _VP]),
+    "mmfd_deberta_rel_bias": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _I64, _VP, _VP, _F, _VP, _VP]),
+    "mmfd_mask_rows": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _VP]),
+    "mmfd_attn_fill_masked_rows": (_I, [_I, _I64, _I64, _I64, _I64, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP]),
     "mmfd_patchify": (_I, [_I, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _VP]),
     "mmfd_vit_tokens_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
     "mmfd_vit_tokens_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
@@ -392,12 +396,59 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
     a.o, a.o_sb, a.o_st = _head_view(out, H, D)
     a.lse = lse.data_ptr()
     a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias = rel_bias.data_ptr() if rel_bias is not None else None
+    a.rel_bias, a.rel_bias_sb = _rel_bias_args(rel_bias, B, H, Lq, Lk)
     a.dropout_p = float(dropout_p)
     a.seed = seed.t.data_ptr() if seed is not None else None
     a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
     _check(lib().mmfd_attn_fwd(ctypes.byref(a), _stream()), "mmfd_attn_fwd")
     return out, lse
+
+
+def _rel_bias_args(rel_bias, B, H, Lq, Lk):
+    """(pointer, batch stride) for an additive fp32 bias shared by the batch ([H, Lq, Lk], MPNet)
+    or per batch row ([B, H, Lq, Lk], DeBERTa)"""
+    if rel_bias is None:
+        return None, 0
+    if rel_bias.dtype != torch.float32 or not rel_bias.is_contiguous():
+        raise ValueError("rel_bias must be a contiguous fp32 tensor")
+    if tuple(rel_bias.shape) == (H, Lq, Lk):
+        return rel_bias.data_ptr(), 0
+    if tuple(rel_bias.shape) == (B, H, Lq, Lk):
+        return rel_bias.data_ptr(), H * Lq * Lk
+    raise ValueError(f"rel_bias shape {tuple(rel_bias.shape)} is neither [H,Lq,Lk] nor [B,H,Lq,Lk]")
+
+
+def deberta_rel_bias(c2p, p2c, c2p_idx, p2c_idx, B, L, inv_scale, out=None):
+    """DeBERTa c2p + p2c bias [B, H, L, L] fp32 from the per-head position scores c2p / p2c
+    ([H, B*L, ld]) and the clamped log-bucket indices (int32 [L, L])."""
+    _require_cuda(c2p, p2c, c2p_idx, p2c_idx)
+    H, _, ld = c2p.shape
+    out = out if out is not None else torch.empty((B, H, L, L), device=c2p.device, dtype=torch.float32)
+    _check(lib().mmfd_deberta_rel_bias(dtype_code(c2p.dtype), B, H, L, _ptr(c2p), _ptr(p2c), ld, _ptr(c2p_idx),
+                                       _ptr(p2c_idx), float(inv_scale), _ptr(out), _stream()), "mmfd_deberta_rel_bias")
+    return out
+
+
+def mask_rows(x2d, mask):
+    """x[r, :] = 0 where mask[r] == 0 (in place)"""
+    _require_cuda(x2d, mask)
+    m = mask.reshape(-1).to(torch.int64).contiguous()
+    _check(lib().mmfd_mask_rows(dtype_code(x2d.dtype), x2d.shape[0], x2d.shape[1], _ptr(x2d), _ld(x2d), _ptr(m),
+                                _stream()), "mmfd_mask_rows")
+    return x2d
+
+
+def attn_fill_masked_rows(v, o, H, mask):
+    """o rows of fully masked queries (mask[b, i] == 0) = mean of v over all keys (in place)"""
+    _require_cuda(v, o, mask)
+    B, L, HD = v.shape
+    Dh = HD // H
+    m = mask.to(torch.int64).contiguous()
+    vp, vsb, vst = _head_view(v, H, Dh)
+    op, osb, ost = _head_view(o, H, Dh)
+    _check(lib().mmfd_attn_fill_masked_rows(dtype_code(v.dtype), B, H, L, Dh, vp, vsb, vst, op, osb, ost, _ptr(m),
+                                            _stream()), "mmfd_attn_fill_masked_rows")
+    return o
 
 
 def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None, key_bias=None, rel_bias=None,
@@ -420,7 +471,7 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
     a.o, a.o_sb, a.o_st = _head_view(o, H, D)
     a.lse = lse.data_ptr()
     a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias = rel_bias.data_ptr() if rel_bias is not None else None
+    a.rel_bias, a.rel_bias_sb = _rel_bias_args(rel_bias, B, H, Lq, k.shape[1])
     a.dropout_p = float(dropout_p)
     a.seed = seed.t.data_ptr() if seed is not None else None
     a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF

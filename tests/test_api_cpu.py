@@ -95,3 +95,22 @@ def test_dropout_hash_statistics():
     a = keep_mask(7, salt_of("a"), (n,), 0.5).astype(np.float64)
     b = keep_mask(7, salt_of("b"), (n,), 0.5).astype(np.float64)
     assert abs(np.corrcoef(a, b)[0, 1]) < 5 / n ** 0.5
+
+
+def test_deberta_host_buckets_and_names():
+    """the product's host-side log buckets equal the oracle's torch restatement of
+    make_log_bucket_position at every length up to 512, and DebertaV2Model carries the
+    transformers DebertaV2Model state_dict names and shapes (a hub checkpoint loads unchanged)"""
+    import numpy as np
+    from transformers import DebertaV2Config as HC, DebertaV2Model as HM
+
+    from mmfd.deberta import DebertaV2Config, DebertaV2Model, log_bucket_relative_positions
+    from oracle.deberta import log_bucket_relative_positions as ref
+    for L in (1, 7, 128, 300, 512):
+        assert np.array_equal(log_bucket_relative_positions(L, 256, 512), ref(L, 256, 512))
+    kw = dict(vocab_size=1000, hidden_size=64, num_hidden_layers=2, num_attention_heads=2, intermediate_size=128)
+    ours = DebertaV2Model(DebertaV2Config(**kw)).state_dict()
+    hf = HM(HC(max_position_embeddings=512, relative_attention=True, position_buckets=256, norm_rel_ebd="layer_norm",
+               share_att_key=True, pos_att_type=["p2c", "c2p"], position_biased_input=False, type_vocab_size=0,
+               **kw)).state_dict()
+    assert {k: tuple(v.shape) for k, v in ours.items()} == {k: tuple(v.shape) for k, v in hf.items()}

@@ -254,3 +254,23 @@ def test_preprocess_oracle_matches_torch_tensor_ops_and_size_rules():
     t = torch.from_numpy(img.copy()).permute(2, 0, 1).contiguous().to(torch.float32).div(255)
     t = t.sub_(torch.tensor([0.485, 0.456, 0.406])[:, None, None]).div_(torch.tensor([0.229, 0.224, 0.225])[:, None, None])
     assert np.array_equal(got, t.numpy())
+
+
+def test_deberta_oracle_matches_transformers_fixture():
+    """oracle/deberta.py (DeBERTa-v3, the reference's default text encoder) against transformers'
+    DebertaV2Model output in tests/golden/deberta_small.npz (L=300 with a padded row)."""
+    from oracle.deberta import deberta_forward
+    z = np.load(os.path.join(G, "deberta_small.npz"))
+    P = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")}
+    out = deberta_forward(P, torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"]),
+                          num_layers=2, num_heads=2)
+    assert (out - torch.from_numpy(z["last_hidden_state"])).abs().max().item() < 1e-5
+
+
+def test_deberta_log_buckets():
+    """make_log_bucket_position: identity inside +-mid, odd-symmetric, within +-(S-1) up to L=512"""
+    from oracle.deberta import log_bucket_relative_positions
+    r = log_bucket_relative_positions(512, 256, 512)
+    assert (r == -r.T).all()
+    assert r[200, 100] == 100 and r[0, 127] == -127
+    assert np.abs(r).max() <= 255
