@@ -4,7 +4,7 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency|preembed]
 """
 import argparse
 import json
@@ -385,6 +385,62 @@ def latency_main(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def preembed_main(args, dev, world, rank):
+    """SURVEY §8(f) row 1, text side: the pre-embedding pass of preprocess_embeddings.py:63-80 —
+    DeBERTa-v3-xsmall (the reference's text encoder) over texts padded to max_length 512, eval, no
+    grad; a step = `--batch` sequences (default 64) resident in HBM. Each rank embeds its own shard
+    of the corpus (no collective). Algorithmic work per sequence at L=512: 12 x (QKV 3LD^2 + out
+    LD^2 + FFN 2LDI + attention 2L^2D + c2p/p2c 2L(2S)D) x 2 FLOP = 31.4 GFLOP (the per-batch
+    projections of the 512 relative embeddings excluded)."""
+    from mmfd.deberta import DebertaV2Config, DebertaV2Model
+
+    L = 512
+    B = args.batch
+    torch.manual_seed(42 + rank)
+    m = DebertaV2Model(DebertaV2Config()).to(dev).eval().set_precision(args.precision)
+    g = torch.Generator(device="cpu").manual_seed(9 + rank)
+    ids = torch.randint(1, 128100, (B, L), generator=g)
+    n = torch.randint(32, L + 1, (B,), generator=g)
+    mask = (torch.arange(L)[None] < n[:, None]).long()
+    ids, mask = (ids * mask).to(dev), mask.to(dev)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            m(input_ids=ids, attention_mask=mask)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            m(input_ids=ids, attention_mask=mask)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    if rank == 0:
+        D, I, S = 384, 1536, 256
+        flops = 12 * (3 * L * D * D + L * D * D + 2 * L * D * I + 2 * L * L * D + 2 * L * 2 * S * D) * 2
+        seqs = B * world * args.steps / elapsed
+        tf = seqs / world * flops / 1e12
+        out = {"metric": "texts/sec embedded (DeBERTa-v3-xsmall, max_length 512, pre-embedding pass)",
+               "value": round(seqs, 1), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+               "data": "synthetic token ids (ragged 32..512 real tokens, padded to 512), random-init weights",
+               "config": {"workload": "pre-embedding text pass (SURVEY 8f row 1): deberta-v3-xsmall forward",
+                          "global_batch": B * world, "seq_len": L, "parallelism": f"shard{world}"},
+               "step_tflops_per_gpu": round(tf, 1), "step_mfma_frac": round(tf / PEAK_TFLOPS[args.precision], 4),
+               "algorithmic_gflop_per_sequence": round(flops / 1e9, 2)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -394,7 +450,8 @@ def main():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess", "latency"],
+    ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess", "latency",
+                                                  "preembed"],
                     default="train")
     args = ap.parse_args()
 
@@ -425,6 +482,10 @@ def main():
         return preprocess_main(args, dev, world, rank)
     if args.workload == "latency":
         return latency_main(args, dev, world, rank)
+    if args.workload == "preembed":
+        if args.batch == 256:
+            args.batch = 64
+        return preembed_main(args, dev, world, rank)
     tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 

@@ -489,7 +489,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 // it: no per-block restaging, no repeated K/V reads from L2, and the forward softmax is single pass
 // (all 16 S^T subtiles stay in registers, so no online rescaling).
 // =================================================================================================
-constexpr int V2_LMAX = 256;
+constexpr int V2_LMAX = 256;      // backward kernels (Q/dO or K/V images of the head)
+constexpr int V2_LMAX_FWD = 512;  // forward: K/V images of 512 keys (128 KB at D = 64) still fit the 160-KB LDS
 constexpr int V2_THREADS = 512;       // forward / dQ: 8 waves sharing one K/V image
 constexpr int V2_DKDV_THREADS = 256;
 template <int D> struct V2 { static constexpr bool DUAL = (D == 64); };  // row image == transposed image
@@ -873,7 +874,7 @@ void launch_fwd_v2(const AttnP& p, hipStream_t s) {
   const int lk_pad = (int)((p.Lk + 63) & ~63);
   const int lds = 2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4;
   static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>),
-                                      2 * V2_LMAX * AT<bf16, D>::RB + V2_LMAX * 4), true);
+                                      2 * V2_LMAX_FWD * AT<bf16, D>::RB + V2_LMAX_FWD * 4), true);
   (void)once;
   hipLaunchKernelGGL((attn_fwd_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds, s, p);
 }
@@ -926,7 +927,10 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const bool v2 = a->dtype == MMFD_BF16 && p.Lk <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  // one workgroup per (b, h): past 256 keys only when there are enough heads to fill the chip (a
+  // batch-1 pair at L = 512 runs faster on the 64-query-block streaming kernel)
+  const bool v2 = a->dtype == MMFD_BF16 && (p.Lk <= V2_LMAX || (p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) &&
+                  !getenv("MMFD_ATTN_V1");
   if (v2) { if (a->D > 32) launch_fwd_v2<64>(p, s); else launch_fwd_v2<32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }

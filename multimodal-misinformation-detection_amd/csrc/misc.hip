@@ -548,19 +548,41 @@ extern "C" int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, flo
 // DeBERTa-v3 helpers (transformers modeling_deberta_v2.py; the reference's default text encoder)
 // ---------------------------------------------------------------------------------------------
 namespace {
-// one thread per (b, h, i, j), j fastest (coalesced fp32 output rows); the c2p gather stays inside
-// row (b, i) of head h, the p2c gather walks rows (b, j)
+// tile of 32 query rows x 64 keys of one (b, h). The p2c gather reads, for a fixed key j, the
+// scores p2c[j][idx(i, j)] of 32 consecutive rows i: idx is monotone in i, so those are one short
+// contiguous run (lanes over i, coalesced) and go through an LDS transpose; the c2p gather
+// (row i, lanes over j) and the fp32 output row are coalesced directly.
+constexpr int RB_TI = 32, RB_TJ = 64;
 template <typename T>
-__global__ void deberta_rel_bias_kernel(int64_t B, int64_t H, int64_t L, const T* __restrict__ c2p,
-                                        const T* __restrict__ p2c, int64_t ld, const int32_t* __restrict__ c2p_idx,
-                                        const int32_t* __restrict__ p2c_idx, float inv_scale, float* __restrict__ out) {
-  const int64_t total = B * H * L * L;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = e % L, i = (e / L) % L, h = (e / (L * L)) % H, b = e / (L * L * H);
-    const int64_t hb = h * B * L + b * L;
+__global__ void __launch_bounds__(256) deberta_rel_bias_kernel(int64_t B, int64_t H, int64_t L, const T* __restrict__ c2p,
+                                                               const T* __restrict__ p2c, int64_t ld,
+                                                               const int32_t* __restrict__ c2p_idx,
+                                                               const int32_t* __restrict__ p2c_idx, float inv_scale,
+                                                               float* __restrict__ out) {
+  __shared__ float tp[RB_TI][RB_TJ + 1];
+  const int64_t j0 = (int64_t)blockIdx.x * RB_TJ, i0 = (int64_t)blockIdx.y * RB_TI;
+  const int64_t bh = blockIdx.z, b = bh / H, h = bh % H;
+  const int64_t hb = h * B * L + b * L;
+  const int t = threadIdx.x;
+  {
+    const int il = t % RB_TI;
+    const int64_t i = i0 + il;
+    for (int jl = t / RB_TI; jl < RB_TJ; jl += 256 / RB_TI) {
+      const int64_t j = j0 + jl;
+      float v = 0.f;
+      if (i < L && j < L) v = to_f32(p2c[(hb + j) * ld + p2c_idx[j * L + i]]);
+      tp[il][jl] = v;
+    }
+  }
+  __syncthreads();
+  const int jl = t % RB_TJ;
+  const int64_t j = j0 + jl;
+  if (j >= L) return;
+  for (int il = t / RB_TJ; il < RB_TI; il += 256 / RB_TJ) {
+    const int64_t i = i0 + il;
+    if (i >= L) break;
     const float c = to_f32(c2p[(hb + i) * ld + c2p_idx[i * L + j]]);
-    const float q = to_f32(p2c[(hb + j) * ld + p2c_idx[j * L + i]]);
-    out[e] = c * inv_scale + q * inv_scale;  // score += c2p / scale; score += p2c / scale (:329, :345)
+    out[(bh * L + i) * L + j] = c * inv_scale + tp[il][jl] * inv_scale;  // score += c2p / s; += p2c / s (:329, :345)
   }
 }
 
@@ -595,9 +617,9 @@ __global__ void __launch_bounds__(256) attn_fill_masked_rows_kernel(int64_t H, i
     for (int64_t t = rg; t < L; t += 4) s += to_f32(v[b * v_sb + t * v_st + h * Dh + d]);
   part[rg][d] = s;
   __syncthreads();
-  if (rg == 0 && d < Dh) {
+  if (d < Dh) {  // every row group writes a quarter of the masked rows
     const T mean = from_f32<T>((part[0][d] + part[1][d] + part[2][d] + part[3][d]) / (float)L);
-    for (int64_t i = 0; i < L; ++i)
+    for (int64_t i = rg; i < L; i += 4)
       if (mask[b * L + i] == 0) o[b * o_sb + i * o_st + h * Dh + d] = mean;
   }
 }
@@ -612,11 +634,13 @@ extern "C" int mmfd_deberta_rel_bias(int dtype, int64_t B, int64_t H, int64_t L,
   if (total == 0) return 0;
   MMFD_CHECK_ARG(c2p && p2c && c2p_idx && p2c_idx && out, "deberta_rel_bias: null pointer");
   hipStream_t s = (hipStream_t)stream;
+  MMFD_CHECK_ARG(B * H < 65536 && L < (1 << 20), "deberta_rel_bias: grid too large");
+  const dim3 grid((unsigned)((L + RB_TJ - 1) / RB_TJ), (unsigned)((L + RB_TI - 1) / RB_TI), (unsigned)(B * H));
   if (dtype == MMFD_BF16)
-    hipLaunchKernelGGL((deberta_rel_bias_kernel<bf16>), dim3(gridn(total, 256)), dim3(256), 0, s, B, H, L,
+    hipLaunchKernelGGL((deberta_rel_bias_kernel<bf16>), grid, dim3(256), 0, s, B, H, L,
                        (const bf16*)c2p, (const bf16*)p2c, ld, c2p_idx, p2c_idx, inv_scale, out);
   else
-    hipLaunchKernelGGL((deberta_rel_bias_kernel<float>), dim3(gridn(total, 256)), dim3(256), 0, s, B, H, L,
+    hipLaunchKernelGGL((deberta_rel_bias_kernel<float>), grid, dim3(256), 0, s, B, H, L,
                        (const float*)c2p, (const float*)p2c, ld, c2p_idx, p2c_idx, inv_scale, out);
   MMFD_CHECK_LAUNCH("deberta_rel_bias");
   return 0;

@@ -219,7 +219,8 @@ def _attn_ref(q, k, v, H, scale, key_bias=None, keep=None, p=0.0):
 
 ATTN_CASES = [(2, 4, 128, 128, 64), (2, 8, 197, 197, 32), (3, 2, 13, 29, 64), (2, 8, 128, 197, 32),
               (1, 12, 70, 70, 64), (2, 4, 21, 33, 8), (2, 2, 40, 40, 16), (1, 3, 65, 130, 48),
-              (1, 2, 260, 300, 64), (2, 16, 256, 256, 64)]  # L > 256 exercises the streaming kernels
+              (1, 2, 260, 300, 64), (2, 16, 256, 256, 64),  # L > 256: streaming backward kernels
+              (1, 2, 512, 512, 64)]  # bf16 forward keeps up to 512 keys resident
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -262,6 +263,59 @@ def test_attention_fwd_bwd(dtype, case, masked, p):
     _close(dq, qr.grad, dtype)
     _close(dk, kr.grad, dtype)
     _close(dv, vr.grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("L", [96, 300])
+def test_attention_batch_strided_rel_bias(dtype, L):
+    """additive bias per batch row [B, H, L, L] (DeBERTa c2p + p2c) next to the key mask, against
+    a float64 softmax reference; the shared [H, L, L] form (MPNet) is the rel_bias_sb = 0 case"""
+    B, H, D = 2, 3, 64
+    q = _rand(B, L, H * D, dtype=dtype, seed=60)
+    k = _rand(B, L, H * D, dtype=dtype, seed=61)
+    v = _rand(B, L, H * D, dtype=dtype, seed=62)
+    rb = _rand(B, H, L, L, seed=63)
+    mask = torch.ones(B, L, dtype=torch.long)
+    mask[1, L // 3:] = 0
+    kb = K.mask_to_bias(mask.to(DEV))
+    scale = (3 * D) ** -0.5
+    o, _ = K.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), H, scale=scale, key_bias=kb, rel_bias=rb.to(DEV))
+    torch.cuda.synchronize()
+    qh = q.double().view(B, L, H, D).transpose(1, 2)
+    kh = k.double().view(B, L, H, D).transpose(1, 2)
+    vh = v.double().view(B, L, H, D).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale + rb.double() + kb.double().cpu()[:, None, None, :]
+    ref = (torch.softmax(s, -1) @ vh).transpose(1, 2).reshape(B, L, H * D)
+    _close(o, ref, dtype)
+
+
+def test_deberta_bias_kernels():
+    """mmfd_deberta_rel_bias (tiled gather of c2p / p2c at host indices), mmfd_mask_rows and
+    mmfd_attn_fill_masked_rows against their definitions"""
+    B, H, L, S = 2, 3, 150, 64
+    c2p = _rand(H, B * L, 2 * S, seed=70)
+    p2c = _rand(H, B * L, 2 * S, seed=71)
+    g = torch.Generator().manual_seed(72)
+    ci = torch.randint(0, 2 * S, (L, L), generator=g, dtype=torch.int32)
+    pi = torch.randint(0, 2 * S, (L, L), generator=g, dtype=torch.int32)
+    out = K.deberta_rel_bias(c2p.to(DEV), p2c.to(DEV), ci.to(DEV), pi.to(DEV), B, L, 0.125)
+    torch.cuda.synchronize()
+    cb = c2p.view(H, B, L, 2 * S).permute(1, 0, 2, 3)  # [B,H,L,2S]
+    pb = p2c.view(H, B, L, 2 * S).permute(1, 0, 2, 3)
+    ref = torch.gather(cb, -1, ci.long().expand(B, H, L, L)) * 0.125 + \
+        torch.gather(pb, -1, pi.long().expand(B, H, L, L)).transpose(-1, -2) * 0.125
+    assert (out.cpu() - ref).abs().max().item() < 1e-6
+    x = _rand(B * L, 40, seed=73).to(DEV)
+    m = (torch.rand(B * L, generator=g) > 0.3).long()
+    y = K.mask_rows(x.clone(), m.to(DEV))
+    assert torch.equal(y.cpu(), x.cpu() * m[:, None])
+    v = _rand(B, L, H * 32, seed=74)
+    o = _rand(B, L, H * 32, seed=75)
+    mk = torch.ones(B, L, dtype=torch.long)
+    mk[1, 100:] = 0
+    of = K.attn_fill_masked_rows(v.to(DEV), o.clone().to(DEV), H, mk.to(DEV)).cpu()
+    assert torch.equal(of[0], o[0]) and torch.equal(of[1, :100], o[1, :100])
+    assert (of[1, 100:] - v[1].mean(0)).abs().max().item() < 1e-5
 
 
 # ---------------------------------------------------------------------------------------------
