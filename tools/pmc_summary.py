@@ -59,6 +59,9 @@ def short_name(name):
     """'void (anonymous namespace)::gemm_mfma_kernel<__bf16, 0, 0, __bf16>(...)' -> 'gemm_mfma_kernel<__bf16, 0, 0, __bf16>'"""
     if name.startswith("_Z"):
         name = _demangle_anon(name)
+    # rocprofv3's own demangler turns the bf16 + bool template pair DF16b Lb1E into
+    # "bool _Accum, bool, E" (the false case stays mangled and is decoded above)
+    name = name.replace("bool _Accum, bool, E>", "__bf16, true>")
     n = re.sub(r"^void\s+", "", name)
     n = n.replace("(anonymous namespace)::", "")
     depth, out = 0, []
