@@ -129,6 +129,8 @@ typedef struct mmfd_attn_args {
   int accumulate_dq;               /* 1: dq += result (else overwrite) */
   int accumulate_dkv;              /* 1: dk += ..., dv += ... */
   int64_t rel_bias_sb;             /* batch stride of rel_bias in floats (0 = shared by the batch) */
+  int64_t rel_bias_mod;            /* > 0: batch row b reads bias row b % rel_bias_mod (Swinv2 windows:
+                                      [nW][H][L][L] shift masks, batch = images x nW windows) */
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);
@@ -141,6 +143,12 @@ int mmfd_attn_bwd(const mmfd_attn_args* args, mmfd_stream_t stream);
 int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
                        const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
                        float* mean, float* rstd, mmfd_stream_t stream);
+/* y = res + LN(x) (Swinv2's res-post-norm, modeling_swinv2.py Swinv2Layer.forward:
+ * `shortcut + layernorm_before(attn)` and `h + layernorm_after(mlp)`); 16-B aligned rows;
+ * mean/rstd may both be NULL (inference). */
+int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
+                           const float* gamma, const float* beta, float eps, const void* res, int64_t ldr,
+                           void* y, int64_t ldy, float* mean, float* rstd, mmfd_stream_t stream);
 /* dx = LN'(dy) (+ dx_add); dgamma/dbeta (fp32, [width]) are written (beta_acc=0) or accumulated
  * (beta_acc=1) through a deterministic two-pass reduction; workspace >= 8*width*256 bytes.
  * If dx_drop != NULL it also receives dropout(dx) for call-site (seed, salt, p) with element
@@ -256,6 +264,28 @@ int mmfd_vit_tokens_fwd(int dtype, int64_t B, int64_t NP, int64_t D, const void*
 int mmfd_vit_tokens_bwd(int dtype, int64_t B, int64_t NP, int64_t D, const void* dout, void* dpatch,
                         float* dcls, float* dpos, void* workspace, int64_t workspace_bytes,
                         mmfd_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------- */
+/* Swinv2 image encoder (reference default image encoder: Swinv2Model swinv2-base-patch4-window8- */
+/* 256, train.py:332, called at train.py:142-143 / preprocess_embeddings.py:91-92; transformers  */
+/* modeling_swinv2.py). Inference only.                                                        */
+/* ------------------------------------------------------------------------------------------- */
+/* dst row (b, r) = concat_g src row (b, idx[r*G + g]); rows are row_bytes wide (multiple of 16).
+ * Replaces torch.roll + window_partition / window_reverse and the patch-merging 2x2 concat. */
+int mmfd_row_gather(int64_t B, int64_t rows_out, int64_t G, int64_t row_bytes, int64_t src_rows,
+                    const void* src, const int32_t* idx, void* dst, mmfd_stream_t stream);
+/* continuous position-bias MLP: out[t][h] = sum_k w2[h][k] relu(w1[k] . coords[t] + b1[k]),
+ * 512 hidden units (Swinv2SelfAttention.continuous_position_bias_mlp), all fp32 */
+int mmfd_swin_cpb(int64_t T, int64_t H, const float* coords, const float* w1, const float* b1,
+                  const float* w2, float* out, mmfd_stream_t stream);
+/* out[w][h][i][j] = 16 sigmoid(table[rpi[i*L+j]][h]) (+ mask[w][i][j] twice, as HF adds it);
+ * mask NULL -> nW must be 1 */
+int mmfd_swin_bias(int64_t nW, int64_t H, int64_t L, const float* table, const int32_t* rpi,
+                   const float* mask, float* out, mmfd_stream_t stream);
+/* cosine attention operands in place on packed [rows][ld] QKV (q at column 0, k at H*d):
+ * q_h /= max(|q_h|, 1e-12) and *= exp(min(logit_scale[h], max_log)); k_h /= max(|k_h|, 1e-12) */
+int mmfd_swin_qk_norm(int dtype, int64_t rows, int64_t H, int64_t d, void* qkv, int64_t ld,
+                      const float* logit_scale, float max_log, mmfd_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------- */
 /* AdamW (torch.optim.AdamW defaults as used at train.py:356/188), multi-tensor, one launch.    */

@@ -146,12 +146,15 @@ class StepCtx:
                     r += w.shape[0]
                 if self.dt != torch.float32:
                     self._register(key, t, wn)
-            bs = [self.P[n + ".bias"] for n in names]
             bt = torch.empty(rows, device=ws[0].device, dtype=torch.float32)
             r = 0
-            for bb in bs:
-                K.cast(bb, torch.float32, out=bt[r:r + bb.shape[0]])
-                r += bb.shape[0]
+            for n, w in zip(names, ws):
+                bb = self.P.get(n + ".bias")
+                if bb is None:   # bias-free projection (Swinv2 key): zero slice of the packed bias
+                    bt[r:r + w.shape[0]].zero_()
+                else:
+                    K.cast(bb, torch.float32, out=bt[r:r + bb.shape[0]])
+                r += w.shape[0]
             self._w[key] = t
             self._w[key + "#bias"] = bt
         return t, self._w[key + "#bias"]

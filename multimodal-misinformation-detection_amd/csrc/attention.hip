@@ -32,7 +32,7 @@ struct AttnP {
   void* o; int64_t o_sb, o_st;
   float* lse;
   const float* key_bias;
-  const float* rel_bias; int64_t rb_sb;
+  const float* rel_bias; int64_t rb_sb, rb_mod;
   float p; uint32_t thr; float keep_scale;
   const uint64_t* seed; uint64_t salt;
   const void* dout; int64_t do_sb, do_st;
@@ -151,10 +151,16 @@ __device__ __forceinline__ void load_row_regs(uint4* f, const T* __restrict__ ba
   }
 }
 
+// batch offset of rel_bias: b * sb, or (b % mod) * sb when the bias repeats every `mod` batch rows
+// (Swinv2 shifted-window masks: one [H][L][L] bias per window position, windows batch-major)
+__device__ __forceinline__ int64_t rb_off(const AttnP& p, int64_t b) {
+  return (p.rb_mod > 0 ? b % p.rb_mod : b) * p.rb_sb;
+}
+
 __device__ __forceinline__ float bias_at(const AttnP& p, int64_t b, int64_t h, int64_t q, int64_t key) {
   float v = 0.f;
   if (p.key_bias) v += p.key_bias[b * p.Lk + key];
-  if (p.rel_bias) v += p.rel_bias[b * p.rb_sb + (h * p.Lq + q) * p.Lk + key];
+  if (p.rel_bias) v += p.rel_bias[rb_off(p, b) + (h * p.Lq + q) * p.Lk + key];
   return v;
 }
 
@@ -551,7 +557,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
     for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
     load_row_regs<T, D>(qn, qb, p.q_st, q0 + V2_THREADS / 4 + li, p.Lq, lane, p.D);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
-    const float* relrow = p.rel_bias ? p.rel_bias + b * p.rb_sb + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
+    const float* relrow = p.rel_bias ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[C::DT];
 #pragma unroll
@@ -700,7 +706,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
         for (int r = 0; r < 4; ++r) {
           const int lq = qs * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kb2);
-          if (p.rel_bias && lq < p.Lq && mykey < p.Lk) t = fmaf(p.rel_bias[b * p.rb_sb + (h * p.Lq + lq) * p.Lk + mykey], LOG2E, t);
+          if (p.rel_bias && lq < p.Lq && mykey < p.Lk) t = fmaf(p.rel_bias[rb_off(p, b) + (h * p.Lq + lq) * p.Lk + mykey], LOG2E, t);
           const float pr = __builtin_amdgcn_exp2f(t - lq2[r]);
           float z = 1.f;
           if (p.p > 0.f) {
@@ -776,7 +782,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
     const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
-    const float* relrow = p.rel_bias ? p.rel_bias + b * p.rb_sb + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
+    const float* relrow = p.rel_bias ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -853,6 +859,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.v = a.v; p.v_sb = a.v_sb; p.v_st = a.v_st;
   p.o = a.o; p.o_sb = a.o_sb; p.o_st = a.o_st;
   p.lse = a.lse; p.key_bias = a.key_bias; p.rel_bias = a.rel_bias; p.rb_sb = a.rel_bias ? a.rel_bias_sb : 0;
+  p.rb_mod = a.rel_bias ? a.rel_bias_mod : 0;
   p.p = a.dropout_p > 0.f ? a.dropout_p : 0.f; p.thr = mmfd_drop_threshold(p.p);
   p.keep_scale = 1.0f / (1.0f - p.p); p.seed = a.seed; p.salt = a.salt;
   p.dout = a.dout; p.do_sb = a.do_sb; p.do_st = a.do_st;

@@ -203,7 +203,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, const T* __restrict__ x, int64_t ldx,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, T* __restrict__ y, int64_t ldy,
-                                                       float* __restrict__ mean, float* __restrict__ rstd) {
+                                                       float* __restrict__ mean, float* __restrict__ rstd,
+                                                       const T* __restrict__ res = nullptr, int64_t ldr = 0) {
   constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -239,10 +240,16 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, 
       load_f32xN<T>(beta + N * c, bb);
 #pragma unroll
       for (int e = 0; e < N; ++e) o[e] = (v[j][e] - mu) * rs * gg[e] + bb[e];
+      if (res) {  // y = res + LN(x) (Swinv2 res-post-norm)
+        float r[N];
+        VN<T>::load(res + row * ldr + N * c, r);
+#pragma unroll
+        for (int e = 0; e < N; ++e) o[e] += r[e];
+      }
       VN<T>::store(y + row * ldy + N * c, o);
     }
   }
-  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
 }
 
 template <typename T>
@@ -356,6 +363,30 @@ extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const 
   else
     hipLaunchKernelGGL((ln_fwd_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
   MMFD_CHECK_LAUNCH("layernorm_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
+                                      const float* gamma, const float* beta, float eps, const void* res,
+                                      int64_t ldr, void* y, int64_t ldy, float* mean, float* rstd,
+                                      mmfd_stream_t stream) {
+  const int epc = dtype == MMFD_BF16 ? 8 : 4;
+  MMFD_CHECK_ARG(width > 0 && width <= 1024 && width % epc == 0, "layernorm_res: width %lld unsupported", (long long)width);
+  MMFD_CHECK_ARG(ldx % epc == 0 && ldy % epc == 0 && ldr % epc == 0 && ((uintptr_t)x & 15) == 0 &&
+                     ((uintptr_t)y & 15) == 0 && ((uintptr_t)res & 15) == 0 && ((uintptr_t)gamma & 15) == 0 &&
+                     ((uintptr_t)beta & 15) == 0,
+                 "layernorm_res: 16-B aligned rows required");
+  MMFD_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "layernorm_res: mean and rstd both or neither");
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta,
+                       eps, (bf16*)y, ldy, mean, rstd, (const bf16*)res, ldr);
+  else
+    hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma,
+                       beta, eps, (float*)y, ldy, mean, rstd, (const float*)res, ldr);
+  MMFD_CHECK_LAUNCH("layernorm_fwd_res");
   return 0;
 }
 

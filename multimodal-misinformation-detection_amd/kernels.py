@@ -76,6 +76,7 @@ class AttnArgs(ctypes.Structure):
         ("accumulate_dq", ctypes.c_int),
         ("accumulate_dkv", ctypes.c_int),
         ("rel_bias_sb", ctypes.c_int64),
+        ("rel_bias_mod", ctypes.c_int64),
     ]
 
 
@@ -135,6 +136,11 @@ SIGNATURES = {
     "mmfd_topk": (_I, [_I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _I64, _VP]),
     "mmfd_resize_normalize": (_I, [_I64, _VP, _I64, _I64, _VP, _VP, _I64, _I64, ctypes.POINTER(ctypes.c_float),
                                    ctypes.POINTER(ctypes.c_float), _VP, _VP]),
+    "mmfd_layernorm_fwd_res": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
+    "mmfd_row_gather": (_I, [_I64, _I64, _I64, _I64, _I64, _VP, _VP, _VP, _VP]),
+    "mmfd_swin_cpb": (_I, [_I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "mmfd_swin_bias": (_I, [_I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+    "mmfd_swin_qk_norm": (_I, [_I, _I64, _I64, _I64, _VP, _I64, _VP, _F, _VP]),
 }
 
 _lib = None
@@ -396,7 +402,7 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
     a.o, a.o_sb, a.o_st = _head_view(out, H, D)
     a.lse = lse.data_ptr()
     a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias, a.rel_bias_sb = _rel_bias_args(rel_bias, B, H, Lq, Lk)
+    a.rel_bias, a.rel_bias_sb, a.rel_bias_mod = _rel_bias_args(rel_bias, B, H, Lq, Lk)
     a.dropout_p = float(dropout_p)
     a.seed = seed.t.data_ptr() if seed is not None else None
     a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
@@ -405,17 +411,20 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
 
 
 def _rel_bias_args(rel_bias, B, H, Lq, Lk):
-    """(pointer, batch stride) for an additive fp32 bias shared by the batch ([H, Lq, Lk], MPNet)
-    or per batch row ([B, H, Lq, Lk], DeBERTa)"""
+    """(pointer, batch stride, batch modulus) for an additive fp32 bias shared by the batch
+    ([H, Lq, Lk], MPNet), per batch row ([B, H, Lq, Lk], DeBERTa) or repeating every M batch rows
+    ([M, H, Lq, Lk] with B % M == 0: Swinv2 shifted-window masks, batch = images x M windows)"""
     if rel_bias is None:
-        return None, 0
+        return None, 0, 0
     if rel_bias.dtype != torch.float32 or not rel_bias.is_contiguous():
         raise ValueError("rel_bias must be a contiguous fp32 tensor")
     if tuple(rel_bias.shape) == (H, Lq, Lk):
-        return rel_bias.data_ptr(), 0
+        return rel_bias.data_ptr(), 0, 0
     if tuple(rel_bias.shape) == (B, H, Lq, Lk):
-        return rel_bias.data_ptr(), H * Lq * Lk
-    raise ValueError(f"rel_bias shape {tuple(rel_bias.shape)} is neither [H,Lq,Lk] nor [B,H,Lq,Lk]")
+        return rel_bias.data_ptr(), H * Lq * Lk, 0
+    if rel_bias.dim() == 4 and tuple(rel_bias.shape[1:]) == (H, Lq, Lk) and B % rel_bias.shape[0] == 0:
+        return rel_bias.data_ptr(), H * Lq * Lk, rel_bias.shape[0]
+    raise ValueError(f"rel_bias shape {tuple(rel_bias.shape)} is neither [H,Lq,Lk] nor [M,H,Lq,Lk] with B % M == 0")
 
 
 def deberta_rel_bias(c2p, p2c, c2p_idx, p2c_idx, B, L, inv_scale, out=None):
@@ -471,7 +480,7 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
     a.o, a.o_sb, a.o_st = _head_view(o, H, D)
     a.lse = lse.data_ptr()
     a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias, a.rel_bias_sb = _rel_bias_args(rel_bias, B, H, Lq, k.shape[1])
+    a.rel_bias, a.rel_bias_sb, a.rel_bias_mod = _rel_bias_args(rel_bias, B, H, Lq, k.shape[1])
     a.dropout_p = float(dropout_p)
     a.seed = seed.t.data_ptr() if seed is not None else None
     a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
@@ -498,6 +507,22 @@ def layernorm_fwd(x2d, gamma, beta, eps, out=None):
                                     float(eps), _ptr(y), _ld(y), _ptr(mean), _ptr(rstd), _stream()),
            "mmfd_layernorm_fwd")
     return y, mean, rstd
+
+
+def layernorm_fwd_res(x2d, gamma, beta, eps, res, out=None, stats=False):
+    """y = res + LN(x) (Swinv2 res-post-norm); returns y (and mean, rstd when stats=True)"""
+    _require_cuda(x2d, gamma, beta, res)
+    R, W = x2d.shape
+    if tuple(res.shape) != (R, W) or res.dtype != x2d.dtype:
+        raise ValueError("layernorm_fwd_res: residual must match x in shape and dtype")
+    y = out if out is not None else torch.empty((R, W), device=x2d.device, dtype=x2d.dtype)
+    mean = torch.empty(R, device=x2d.device, dtype=torch.float32) if stats else None
+    rstd = torch.empty(R, device=x2d.device, dtype=torch.float32) if stats else None
+    _check(lib().mmfd_layernorm_fwd_res(dtype_code(x2d.dtype), R, W, _ptr(x2d), _ld(x2d), _ptr(gamma), _ptr(beta),
+                                        float(eps), _ptr(res), _ld(res), _ptr(y), _ld(y),
+                                        _ptr(mean) if stats else None, _ptr(rstd) if stats else None, _stream()),
+           "mmfd_layernorm_fwd_res")
+    return (y, mean, rstd) if stats else y
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None, dbeta=None, beta_acc=0.0,
@@ -773,3 +798,57 @@ def topk(scores, k):
     _check(lib().mmfd_topk(Q, N, _ptr(scores), _ld(scores), k, _ptr(val), _ptr(idx), _ptr(ws), nbytes, _stream()),
            "mmfd_topk")
     return val, idx
+
+
+# -------------------------------------------------------------------------------------------------
+# Swinv2 (csrc/swin.hip)
+# -------------------------------------------------------------------------------------------------
+def row_gather(src, idx, B, rows_out, G=1, out=None):
+    """src [B*src_rows, C] -> out [B*rows_out, G*C] with out row (b, r) = concat_g src row
+    (b, idx[r*G+g]); idx int32 [rows_out*G] (one image's table, shared by the batch)"""
+    _require_cuda(src, idx)
+    if idx.dtype != torch.int32 or idx.numel() != rows_out * G:
+        raise ValueError("row_gather: idx must be int32 [rows_out*G]")
+    if not src.is_contiguous() or src.shape[0] % B:
+        raise ValueError("row_gather: src must be contiguous [B*src_rows, C]")
+    C = src.shape[1]
+    if out is None:
+        out = torch.empty((B * rows_out, G * C), device=src.device, dtype=src.dtype)
+    _check(lib().mmfd_row_gather(B, rows_out, G, C * src.element_size(), src.shape[0] // B, _ptr(src), _ptr(idx),
+                                 _ptr(out), _stream()), "mmfd_row_gather")
+    return out
+
+
+def swin_cpb(coords, w1, b1, w2, out=None):
+    """continuous position-bias MLP table [T, H] (fp32) from coords [T, 2], w1 [512, 2], b1 [512], w2 [H, 512]"""
+    _require_cuda(coords, w1, b1, w2)
+    T, H = coords.shape[0], w2.shape[0]
+    if w1.shape != (512, 2) or w2.shape[1] != 512:
+        raise ValueError("swin_cpb: the position-bias MLP has 512 hidden units")
+    ts = [t.float().contiguous() for t in (coords, w1, b1, w2)]
+    if out is None:
+        out = torch.empty((T, H), device=coords.device, dtype=torch.float32)
+    _check(lib().mmfd_swin_cpb(T, H, *[_ptr(t) for t in ts], _ptr(out), _stream()), "mmfd_swin_cpb")
+    return out
+
+
+def swin_bias(table, rpi, L, mask=None, out=None):
+    """[nW, H, L, L] fp32 = 16 sigmoid(table[rpi]) (+ 2 * mask[nW, L, L]); nW = 1 without a mask"""
+    _require_cuda(table, rpi)
+    H = table.shape[1]
+    nW = mask.shape[0] if mask is not None else 1
+    if out is None:
+        out = torch.empty((nW, H, L, L), device=table.device, dtype=torch.float32)
+    _check(lib().mmfd_swin_bias(nW, H, L, _ptr(table), _ptr(rpi), _ptr(mask) if mask is not None else None,
+                                _ptr(out), _stream()), "mmfd_swin_bias")
+    return out
+
+
+def swin_qk_norm(qkv, H, d, logit_scale, max_log):
+    """in place on packed QKV rows [rows, >= 2*H*d]: cosine-attention q (times the head's clamped
+    exp(logit_scale)) and k"""
+    _require_cuda(qkv, logit_scale)
+    ls = logit_scale.float().contiguous()
+    _check(lib().mmfd_swin_qk_norm(dtype_code(qkv.dtype), qkv.shape[0], H, d, _ptr(qkv), _ld(qkv), _ptr(ls),
+                                   float(max_log), _stream()), "mmfd_swin_qk_norm")
+    return qkv

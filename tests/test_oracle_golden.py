@@ -274,3 +274,37 @@ def test_deberta_log_buckets():
     assert (r == -r.T).all()
     assert r[200, 100] == 100 and r[0, 127] == -127
     assert np.abs(r).max() <= 255
+
+
+SWIN_SMALL = dict(image_size=128, patch_size=4, num_channels=3, embed_dim=32, depths=(2, 2, 2), num_heads=(1, 2, 4),
+                  window_size=8, mlp_ratio=4.0, layer_norm_eps=1e-5, pretrained_window_sizes=(0, 0, 0))
+
+
+def test_swinv2_oracle_matches_transformers_fixture():
+    """oracle/swinv2.py (Swinv2, the reference's default image encoder) against transformers'
+    Swinv2Model in tests/golden/swinv2_small.npz (shifted windows in stages 1-2, one head's
+    logit_scale above the ln(100) clamp): last_hidden_state and pooler_output."""
+    from oracle.swinv2 import swinv2_forward
+    z = np.load(os.path.join(G, "swinv2_small.npz"))
+    P = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")}
+    out, pooled = swinv2_forward(P, torch.from_numpy(z["pixel_values"]), SWIN_SMALL)
+    assert (out - torch.from_numpy(z["last_hidden_state"])).abs().max().item() < 1e-5
+    assert (pooled - torch.from_numpy(z["pooler_output"])).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("R,ws,shift", [(64, 8, 0), (64, 8, 4), (32, 8, 4), (8, 8, 0)])
+def test_swinv2_host_geometry_matches_oracle(R, ws, shift):
+    """the product's host-side tables (mmfd.swinv2: window order as one row permutation, shift mask,
+    coords table / relative position index) equal the oracle's roll + window_partition / mask /
+    create_coords_table_and_index"""
+    import mmfd.swinv2 as S
+    from oracle import swinv2 as O
+    nat = torch.arange(R * R, dtype=torch.float32).view(1, R, R, 1)
+    rolled = torch.roll(nat, shifts=(-shift, -shift), dims=(1, 2)) if shift else nat
+    want = O._partition(rolled, ws).reshape(-1).long().numpy()
+    assert np.array_equal(S.window_order(R, ws, shift), want)
+    if shift:
+        assert np.array_equal(S.shift_mask(R, ws, shift), O._mask(R, R, ws, shift).numpy())
+    t, rpi = S.coords_table_and_index(ws)
+    t2, rpi2 = O._coords(ws, 0)
+    assert torch.equal(t, t2.float()) and torch.equal(rpi.long(), rpi2.reshape(-1))
