@@ -4,7 +4,7 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency|preembed]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency|preembed|preembed_image]
 """
 import argparse
 import json
@@ -441,6 +441,66 @@ def preembed_main(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def preembed_image_main(args, dev, world, rank):
+    """SURVEY §8(f) row 1, image side: the pre-embedding pass of preprocess_embeddings.py:91-92 —
+    Swinv2-base-patch4-window8-256 (the reference's image encoder, train.py:332) over [B,3,256,256]
+    images -> [B,64,1024], eval, no grad; a step = `--batch` images (default 64) resident in HBM.
+    Each rank embeds its own shard (no collective). Algorithmic work per image (printed): per block
+    2 x (12 N C^2 + 4 N L C) FLOP with N tokens, C channels, L = 64 window tokens; per patch merge
+    2 x 2 N C^2; patch embedding 2 x 4096 x 48 x 128."""
+    from mmfd.swinv2 import Swinv2Config, Swinv2Model, stage_geometry
+
+    B = args.batch
+    cfg = Swinv2Config()
+    torch.manual_seed(42 + rank)
+    m = Swinv2Model(cfg).to(dev).eval().set_precision(args.precision)
+    g = torch.Generator(device="cpu").manual_seed(9 + rank)
+    px = torch.randn(B, 3, cfg.image_size, cfg.image_size, generator=g).to(dev)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            m(px)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            m(px)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    if rank == 0:
+        R0 = cfg.image_size // cfg.patch_size
+        flops = 2 * R0 * R0 * 3 * cfg.patch_size ** 2 * cfg.embed_dim
+        geo = stage_geometry(cfg)
+        for i, (R, C, H, blocks) in enumerate(geo):
+            N = R * R
+            for ws, _ in blocks:
+                flops += 2 * (12 * N * C * C + 4 * N * ws * ws * C)
+            if i < len(geo) - 1:
+                flops += 2 * 2 * N * C * C
+        imgs = B * world * args.steps / elapsed
+        tf = imgs / world * flops / 1e12
+        out = {"metric": "images/sec embedded (Swinv2-base-patch4-window8-256, pre-embedding pass)",
+               "value": round(imgs, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+               "data": "synthetic N(0,1) pixels [B,3,256,256], random-init weights",
+               "config": {"workload": "pre-embedding image pass (SURVEY 8f row 1): swinv2-base forward",
+                          "global_batch": B * world, "image_size": cfg.image_size, "parallelism": f"shard{world}"},
+               "step_tflops_per_gpu": round(tf, 1), "step_mfma_frac": round(tf / PEAK_TFLOPS[args.precision], 4),
+               "algorithmic_gflop_per_image": round(flops / 1e9, 2)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,7 +511,7 @@ def main():
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess", "latency",
-                                                  "preembed"],
+                                                  "preembed", "preembed_image"],
                     default="train")
     args = ap.parse_args()
 
@@ -482,6 +542,10 @@ def main():
         return preprocess_main(args, dev, world, rank)
     if args.workload == "latency":
         return latency_main(args, dev, world, rank)
+    if args.workload == "preembed_image":
+        if args.batch == 256:
+            args.batch = 64
+        return preembed_image_main(args, dev, world, rank)
     if args.workload == "preembed":
         if args.batch == 256:
             args.batch = 64

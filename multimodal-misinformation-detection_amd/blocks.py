@@ -63,6 +63,7 @@ class StepCtx:
         self.grad_ready = None   # optional callable(names, grads): finished gradients (DP overlap)
         self._notified = set()
         self.side = None         # stream for weight-gradient GEMMs (enable_side_stream)
+        self.cache_derived = False  # keep weight-derived tensors across calls (see derived())
         self._side_used = False
 
     def enable_side_stream(self, device):
@@ -146,18 +147,37 @@ class StepCtx:
                     r += w.shape[0]
                 if self.dt != torch.float32:
                     self._register(key, t, wn)
-            bt = torch.empty(rows, device=ws[0].device, dtype=torch.float32)
-            r = 0
-            for n, w in zip(names, ws):
-                bb = self.P.get(n + ".bias")
-                if bb is None:   # bias-free projection (Swinv2 key): zero slice of the packed bias
-                    bt[r:r + w.shape[0]].zero_()
-                else:
-                    K.cast(bb, torch.float32, out=bt[r:r + bb.shape[0]])
-                r += w.shape[0]
+            def pack_bias():
+                bt = torch.empty(rows, device=ws[0].device, dtype=torch.float32)
+                r = 0
+                for n, w in zip(names, ws):
+                    bb = self.P.get(n + ".bias")
+                    if bb is None:   # bias-free projection (Swinv2 key): zero slice of the packed bias
+                        bt[r:r + w.shape[0]].zero_()
+                    else:
+                        K.cast(bb, torch.float32, out=bt[r:r + bb.shape[0]])
+                    r += w.shape[0]
+                return bt
             self._w[key] = t
-            self._w[key + "#bias"] = bt
+            self._w[key + "#bias"] = self.derived(key + "#bias", [n + ".bias" for n in names if n + ".bias" in self.P],
+                                                  pack_bias)
         return t, self._w[key + "#bias"]
+
+    def derived(self, key, pnames, make):
+        """a tensor computed from the parameters `pnames` only (packed biases, Swinv2 position-bias
+        tables), kept in the module's persistent store and rebuilt when any of them changed
+        (data pointer or version counter). Opt-in per context (`cache_derived`): only for frozen,
+        inference-only encoders — mmfd's AdamW writes parameters through raw pointers without
+        bumping torch's version counter, so training contexts always rebuild."""
+        if self.shadows is None or not self.cache_derived:
+            return make()
+        sig = tuple((self.P[n].data_ptr(), self.P[n]._version) for n in pnames)
+        ent = self.shadows.get(("derived", key))
+        if ent is not None and ent[0] == sig:
+            return ent[1]
+        t = make()
+        self.shadows[("derived", key)] = (sig, t)
+        return t
 
     # ---- dropout -------------------------------------------------------------------------------
     def drop(self, site):

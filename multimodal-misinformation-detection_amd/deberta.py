@@ -150,6 +150,7 @@ class DebertaV2Model(nn.Module):
                                       "call it under torch.no_grad() or freeze its parameters")
         P = {n: p.detach() for n, p in params.items()}
         ctx = Bk.StepCtx(P, self.compute_dtype, shadows=Bk.shadow_store(self))
+        ctx.cache_derived = True          # frozen encoder: packed QKV biases persist across calls
         out = deberta_forward(self, ctx, input_ids, attention_mask)
         return EncoderOutput(last_hidden_state=out)
 

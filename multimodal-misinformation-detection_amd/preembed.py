@@ -9,8 +9,9 @@ Differences: inputs are pre-tokenised (no tokenizer vocabulary offline; the item
 mmfd.dataset.SyntheticFactifyDataset have the keys used here); claim and document go through each
 encoder as ONE stacked batch; the store is H5 when h5py is importable and otherwise a directory
 with one `<idx>.npz` per sample holding the same datasets (h5py is absent in this image), read
-back by `PreEmbedDataset`. The reference's image encoder is Swinv2-base (window attention), not
-built yet: any mmfd image encoder with `.last_hidden_state` (ViT-B/16) plugs in.
+back by `PreEmbedDataset`. The reference's image encoder, Swinv2-base-patch4-window8-256
+([B,3,256,256] -> [B,64,1024]), is `mmfd.swinv2.Swinv2Model`; any mmfd image encoder with
+`.last_hidden_state` (ViT-B/16) plugs in as well.
 """
 from __future__ import annotations
 

@@ -219,6 +219,7 @@ class Swinv2Model(nn.Module):
         pw = "embeddings.patch_embeddings.projection.weight"
         P[pw] = P[pw].reshape(P[pw].shape[0], -1)               # conv as a [C_out, 3*p*p] GEMM weight
         ctx = Bk.StepCtx(P, self.compute_dtype, shadows=Bk.shadow_store(self))
+        ctx.cache_derived = True          # frozen encoder: packed biases / position-bias tables persist
         geo = self._geo.get(str(first.device))
         if geo is None:
             geo = self._geo[str(first.device)] = _Geo(first.device)
@@ -286,13 +287,14 @@ def _swin_block(ctx, geo, x, pre, B, R, dim, H, d, ws, shift, nW, L, eps, cfg):
     stage = int(pre.split(".")[2])
     pws = cfg.pretrained_window_sizes[stage]
     coords, rpi = geo.get(("cpb", ws, pws), lambda: tuple(t.to(geo.dev) for t in coords_table_and_index(ws, pws)))
-    table = K.swin_cpb(coords, ctx.P[s + ".continuous_position_bias_mlp.0.weight"],
-                       ctx.P[s + ".continuous_position_bias_mlp.0.bias"],
-                       ctx.P[s + ".continuous_position_bias_mlp.2.weight"])
+    cpb = [s + ".continuous_position_bias_mlp.0.weight", s + ".continuous_position_bias_mlp.0.bias",
+           s + ".continuous_position_bias_mlp.2.weight"]
     mask = None
     if shift > 0:
         mask = geo.get(("mask", R, ws, shift), lambda: torch.from_numpy(shift_mask(R, ws, shift)).to(geo.dev))
-    bias = K.swin_bias(table, rpi, L, mask)                  # [nW|1, H, L, L]
+    # [nW|1, H, L, L]: depends on the block's weights only -> rebuilt only when they change
+    bias = ctx.derived(s + "#swin_bias", cpb,
+                       lambda: K.swin_bias(K.swin_cpb(coords, *[ctx.P[n] for n in cpb]), rpi, L, mask))
     q3 = qkv.view(B * nW, L, 3 * dim)
     o, _ = K.attn_fwd(q3[..., :dim], q3[..., dim:2 * dim], q3[..., 2 * dim:], H, scale=1.0,
                       rel_bias=bias if shift > 0 else bias.view(H, L, L))

@@ -154,3 +154,29 @@ def test_swinv2_refuses_grad_and_cpu():
     m = m.cuda()
     with pytest.raises(NotImplementedError):
         m(torch.zeros(1, 3, 128, 128, device="cuda"))
+
+
+def test_swinv2_weight_change_rebuilds_cached_bias():
+    """the per-block position-bias tables and packed QKV biases persist across calls (frozen
+    encoder) and are rebuilt when a weight changes in place"""
+    from mmfd.swinv2 import Swinv2Model
+    from oracle.swinv2 import swinv2_forward
+    z = np.load(os.path.join(G, "swinv2_small.npz"))
+    m = Swinv2Model(_cfg(**SMALL))
+    m.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")})
+    m = m.cuda().eval()
+    px = torch.from_numpy(z["pixel_values"])
+    with torch.no_grad():
+        a = m(px.cuda()).last_hidden_state.clone()
+        b = m(px.cuda()).last_hidden_state
+        assert torch.equal(a, b)
+        blk = m.encoder.layers[0].blocks[1].attention.self
+        blk.continuous_position_bias_mlp[2].weight.mul_(3.0)
+        blk.query.bias.add_(0.5)
+        c = m(px.cuda()).last_hidden_state
+        want, _ = swinv2_forward({k: v.cpu() for k, v in m.state_dict().items()}, px, dict(
+            image_size=128, patch_size=4, num_channels=3, embed_dim=32, depths=(2, 2, 2), num_heads=(1, 2, 4),
+            window_size=8, mlp_ratio=4.0, layer_norm_eps=1e-5, pretrained_window_sizes=(0, 0, 0)))
+    torch.cuda.synchronize()
+    assert (c.cpu() - want).abs().max().item() < 1e-4
+    assert (c - a).abs().max().item() > 1e-3
