@@ -524,38 +524,50 @@ __device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t 
     dst[i] = i < p.Lk ? (p.key_bias ? fmaxf(p.key_bias[b * p.Lk + i] * LOG2E, -1e30f) : 0.f) : -INFINITY;
 }
 
-template <int D>
+template <int D, int HPB = 1>
 __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
-  // domain) over 64-key chunks; key mask/padding come from a per-key bias vector in LDS
+  // domain) over 64-key chunks; key mask/padding come from a per-key bias vector in LDS.
+  // HPB > 1 (short windows: Lq <= 64 / 32, Lk <= 64, e.g. Swinv2's 8x8 windows): the 8 waves split
+  // into HPB groups, each owning one (b, h) with its own LDS images, so no wave idles on a head
+  // that has fewer 16-query blocks than the workgroup has waves.
   using T = bf16;
   using C = AT<T, D>;
+  constexpr int WPH = (V2_THREADS / 64) / HPB;  // waves per head
+  constexpr int TPH = V2_THREADS / HPB;         // threads per head
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sub = wave_all / WPH, wave = wave_all % WPH, htid = tid % TPH;
+  const int64_t nbh = p.B * p.H, bh_raw = (int64_t)blockIdx.x * HPB + sub;
+  const bool active = bh_raw < nbh;
+  const int64_t bh = active ? bh_raw : nbh - 1, b = bh / p.H, h = bh % p.H;
   const int lk_pad = (int)((p.Lk + 63) & ~63);
-  char* k_img = smem;
-  char* v_img = smem + lk_pad * C::RB;
-  float* kbias = reinterpret_cast<float*>(smem + 2 * lk_pad * C::RB);
+  char* hbase = smem + sub * (2 * lk_pad * C::RB + lk_pad * 4);
+  char* k_img = hbase;
+  char* v_img = hbase + lk_pad * C::RB;
+  float* kbias = reinterpret_cast<float*>(hbase + 2 * lk_pad * C::RB);
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
-  stage_all<T, D, false>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, tid, p.D);
-  stage_all<T, D, true>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
-  stage_kbias<V2_THREADS>(kbias, p, b, lk_pad, tid);
+  stage_all<T, D, false, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
+  stage_all<T, D, true, TPH>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, htid, p.D);
+  stage_kbias<TPH>(kbias, p, b, lk_pad, htid);
   __syncthreads();
+  if (!active) return;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
+  const bool rel4 = p.rel_bias && (p.Lk & 3) == 0 && (reinterpret_cast<uintptr_t>(p.rel_bias) & 15) == 0 &&
+                    (p.rb_sb & 3) == 0;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
   uint4 qn[C::KCH];  // next query block's fragments, prefetched one block ahead
   load_row_regs<T, D>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
-  for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
+  for (int qbk = wave; qbk < nqb; qbk += WPH) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH];
 #pragma unroll
     for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
-    load_row_regs<T, D>(qn, qb, p.q_st, q0 + V2_THREADS / 4 + li, p.Lq, lane, p.D);
+    load_row_regs<T, D>(qn, qb, p.q_st, q0 + WPH * 16 + li, p.Lq, lane, p.D);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
     const float* relrow = p.rel_bias ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
@@ -572,6 +584,20 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
         for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
       }
+      float rb[4][4];
+      if (relrow) {  // the 4 keys of a lane are contiguous: one 16-B load per subtile when aligned
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int kk = k0 + ks * 16 + 4 * g;
+          if (rel4) {
+            const float4 v = kk < p.Lk ? *reinterpret_cast<const float4*>(relrow + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[ks][0] = v.x; rb[ks][1] = v.y; rb[ks][2] = v.z; rb[ks][3] = v.w;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rb[ks][r] = kk + r < p.Lk ? relrow[kk + r] : 0.f;
+          }
+        }
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -580,10 +606,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float t = fmaf(s[ks][r], c2, kb[r]);
-          if (relrow) {
-            const int key = k0 + ks * 16 + 4 * g + r;
-            if (key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
-          }
+          if (relrow && k0 + ks * 16 + 4 * g + r < p.Lk) t = fmaf(rb[ks][r], LOG2E, t);
           s[ks][r] = t;
           mx = fmaxf(mx, t);
         }
@@ -876,14 +899,27 @@ void set_lds_attr(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+template <int D, int HPB>
+void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
+  const int lk_pad = (int)((p.Lk + 63) & ~63);
+  const int lds = HPB * (2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4);
+  constexpr int lmax = HPB == 1 ? V2_LMAX_FWD : 64;
+  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D, HPB>),
+                                      HPB * (2 * lmax * AT<bf16, D>::RB + lmax * 4)), true);
+  (void)once;
+  const int64_t nbh = p.B * p.H;
+  hipLaunchKernelGGL((attn_fwd_v2_kernel<D, HPB>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS), lds, s, p);
+}
+
 template <int D>
 void launch_fwd_v2(const AttnP& p, hipStream_t s) {
-  const int lk_pad = (int)((p.Lk + 63) & ~63);
-  const int lds = 2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4;
-  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D>),
-                                      2 * V2_LMAX_FWD * AT<bf16, D>::RB + V2_LMAX_FWD * 4), true);
-  (void)once;
-  hipLaunchKernelGGL((attn_fwd_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds, s, p);
+  // short windows: several heads per workgroup so all 8 waves own a 16-query block
+  if (p.Lk <= 64 && p.Lq <= 32)
+    launch_fwd_v2_hpb<D, 4>(p, s);
+  else if (p.Lk <= 64 && p.Lq <= 64)
+    launch_fwd_v2_hpb<D, 2>(p, s);
+  else
+    launch_fwd_v2_hpb<D, 1>(p, s);
 }
 
 template <int D>
