@@ -252,6 +252,79 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, 
   if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
 }
 
+// narrow rows (width / elements-per-16B <= LPR): 64 / LPR rows per wave, LPR lanes per row, one
+// 16-B chunk per lane, group reductions over the LPR lanes (the one-row-per-wave kernel leaves 3/4
+// of the lanes idle at width 128 bf16: Swinv2 stage 1, and half of them at the fusion head's 256)
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int LPR>
+__global__ void __launch_bounds__(256) ln_fwd16_narrow_kernel(int64_t rows, int width, const T* __restrict__ x,
+                                                              int64_t ldx, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              T* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                                                              float* __restrict__ rstd, const T* __restrict__ res,
+                                                              int64_t ldr) {
+  constexpr int N = VN<T>::N, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, l = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  if (row >= rows) return;  // whole LPR groups leave together: the group shuffles stay inside live lanes
+  const int nch = width / N;
+  const bool on = l < nch;
+  float v[N];
+  float s = 0.f;
+  if (on) {
+    VN<T>::load(x + row * ldx + N * l, v);
+#pragma unroll
+    for (int e = 0; e < N; ++e) s += v[e];
+  }
+  const float mu = group_sum<LPR>(s) / (float)width;
+  float q = 0.f;
+  if (on) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) { const float d = v[e] - mu; q += d * d; }
+  }
+  const float rs = rsqrtf(group_sum<LPR>(q) / (float)width + eps);
+  if (on) {
+    float gg[N], bb[N], o[N];
+    load_f32xN<T>(gamma + N * l, gg);
+    load_f32xN<T>(beta + N * l, bb);
+#pragma unroll
+    for (int e = 0; e < N; ++e) o[e] = (v[e] - mu) * rs * gg[e] + bb[e];
+    if (res) {
+      float r[N];
+      VN<T>::load(res + row * ldr + N * l, r);
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] += r[e];
+    }
+    VN<T>::store(y + row * ldy + N * l, o);
+  }
+  if (l == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// launches the narrow kernel when a row fits 16 / 32 lanes; false -> caller uses the row-per-wave one
+template <typename T>
+bool launch_ln_narrow(hipStream_t s, int64_t rows, int width, const T* x, int64_t ldx, const float* gamma,
+                      const float* beta, float eps, T* y, int64_t ldy, float* mean, float* rstd, const T* res,
+                      int64_t ldr) {
+  const int nch = width / VN<T>::N;
+  if (nch <= 16) {
+    hipLaunchKernelGGL((ln_fwd16_narrow_kernel<T, 16>), dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, rows,
+                       width, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, res, ldr);
+    return true;
+  }
+  if (nch <= 32) {
+    hipLaunchKernelGGL((ln_fwd16_narrow_kernel<T, 32>), dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, rows,
+                       width, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, res, ldr);
+    return true;
+  }
+  return false;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, const T* __restrict__ dy, int64_t lddy,
                                                        const T* __restrict__ x, int64_t ldx, const float* __restrict__ gamma,
@@ -354,7 +427,11 @@ extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const 
   const bool v16 = width % epc == 0 && ldx % epc == 0 && ldy % epc == 0 && ((uintptr_t)x & 15) == 0 &&
                    ((uintptr_t)y & 15) == 0 && ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0;
   if (v16) {
-    if (dtype == MMFD_BF16)
+    if (dtype == MMFD_BF16 ? launch_ln_narrow<bf16>(s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y,
+                                                    ldy, mean, rstd, nullptr, 0)
+                           : launch_ln_narrow<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps,
+                                                     (float*)y, ldy, mean, rstd, nullptr, 0)) {
+    } else if (dtype == MMFD_BF16)
       hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
     else
       hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
@@ -380,7 +457,11 @@ extern "C" int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, co
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
-  if (dtype == MMFD_BF16)
+  if (dtype == MMFD_BF16 ? launch_ln_narrow<bf16>(s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y,
+                                                  ldy, mean, rstd, (const bf16*)res, ldr)
+                         : launch_ln_narrow<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps,
+                                                   (float*)y, ldy, mean, rstd, (const float*)res, ldr)) {
+  } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta,
                        eps, (bf16*)y, ldy, mean, rstd, (const bf16*)res, ldr);
   else
