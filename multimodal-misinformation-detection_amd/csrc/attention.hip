@@ -524,7 +524,7 @@ __device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t 
     dst[i] = i < p.Lk ? (p.key_bias ? fmaxf(p.key_bias[b * p.Lk + i] * LOG2E, -1e30f) : 0.f) : -INFINITY;
 }
 
-template <int D, int HPB = 1>
+template <int D, int HPB, bool REL>
 __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
   // domain) over 64-key chunks; key mask/padding come from a per-key bias vector in LDS.
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
     for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
     load_row_regs<T, D>(qn, qb, p.q_st, q0 + WPH * 16 + li, p.Lq, lane, p.D);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
-    const float* relrow = p.rel_bias ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
+    const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[C::DT];
 #pragma unroll
@@ -584,29 +584,28 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
         for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
       }
-      float rb[4][4];
-      if (relrow) {  // the 4 keys of a lane are contiguous: one 16-B load per subtile when aligned
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int kk = k0 + ks * 16 + 4 * g;
-          if (rel4) {
-            const float4 v = kk < p.Lk ? *reinterpret_cast<const float4*>(relrow + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
-            rb[ks][0] = v.x; rb[ks][1] = v.y; rb[ks][2] = v.z; rb[ks][3] = v.w;
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rb[ks][r] = kk + r < p.Lk ? relrow[kk + r] : 0.f;
-          }
-        }
-      }
       float mx = -INFINITY;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const float4 kb4 = *reinterpret_cast<const float4*>(kbias + k0 + ks * 16 + 4 * g);
         const float kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
+        float rb[4] = {0.f, 0.f, 0.f, 0.f};
+        const int kk = k0 + ks * 16 + 4 * g;
+        if (REL) {  // the 4 keys of a lane are contiguous: one 16-B load per subtile when aligned
+          if (rel4) {
+            if (kk < p.Lk) {
+              const float4 v = *reinterpret_cast<const float4*>(relrow + kk);
+              rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rb[r] = kk + r < p.Lk ? relrow[kk + r] : 0.f;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float t = fmaf(s[ks][r], c2, kb[r]);
-          if (relrow && k0 + ks * 16 + 4 * g + r < p.Lk) t = fmaf(rb[ks][r], LOG2E, t);
+          if (REL && kk + r < p.Lk) t = fmaf(rb[r], LOG2E, t);
           s[ks][r] = t;
           mx = fmaxf(mx, t);
         }
@@ -899,16 +898,27 @@ void set_lds_attr(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-template <int D, int HPB>
+template <int D, int HPB, bool REL>
 void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
   const int lk_pad = (int)((p.Lk + 63) & ~63);
   const int lds = HPB * (2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4);
   constexpr int lmax = HPB == 1 ? V2_LMAX_FWD : 64;
-  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D, HPB>),
+  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D, HPB, REL>),
                                       HPB * (2 * lmax * AT<bf16, D>::RB + lmax * 4)), true);
   (void)once;
   const int64_t nbh = p.B * p.H;
-  hipLaunchKernelGGL((attn_fwd_v2_kernel<D, HPB>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS), lds, s, p);
+  hipLaunchKernelGGL((attn_fwd_v2_kernel<D, HPB, REL>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS), lds,
+                     s, p);
+}
+
+// the relative-bias instantiation carries the extra loads / registers; plain attention (BERT, ViT,
+// fusion head) keeps the bias-free one
+template <int D, int HPB>
+void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
+  if (p.rel_bias)
+    launch_fwd_v2_hpb<D, HPB, true>(p, s);
+  else
+    launch_fwd_v2_hpb<D, HPB, false>(p, s);
 }
 
 template <int D>
