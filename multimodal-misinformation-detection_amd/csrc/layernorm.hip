@@ -413,6 +413,85 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
   }
 }
 
+// narrow rows (width / elements-per-16B <= LPR): 64 / LPR rows per wave, one 16-B chunk per lane;
+// gamma/beta partials of a column chunk are summed over the waves AND the row groups of the block
+template <typename T, int LPR>
+__global__ void __launch_bounds__(256) ln_bwd16_narrow_kernel(int64_t rows, int width, const T* __restrict__ dy,
+                                                              int64_t lddy, const T* __restrict__ x, int64_t ldx,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd, T* __restrict__ dx,
+                                                              int64_t lddx, const T* __restrict__ dx_add, int64_t ldadd,
+                                                              T* __restrict__ dx_drop, float p, uint32_t thr,
+                                                              const uint64_t* __restrict__ seedp, uint64_t salt,
+                                                              float* __restrict__ part) {
+  constexpr int N = VN<T>::N, RPW = 64 / LPR;
+  __shared__ float red[4][2][64 * N];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l = lane % LPR, sub = lane / LPR;
+  const int nch = width / N;
+  const bool on = l < nch;
+  const uint64_t seed = (dx_drop && p > 0.f) ? *seedp : 0ull;
+  const float keep = 1.0f / (1.0f - p);
+  float pg[N], pb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) { pg[e] = 0.f; pb[e] = 0.f; }
+  for (int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RPW + sub; row < rows; row += (int64_t)gridDim.x * 4 * RPW) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[N], g[N], add[N];
+    float s1 = 0.f, s2 = 0.f;
+    if (on) {
+      float d[N], gv[N];
+      VN<T>::load(dy + row * lddy + N * l, d);
+      VN<T>::load(x + row * ldx + N * l, xh);
+      if (dx_add) VN<T>::load(dx_add + row * ldadd + N * l, add);
+      load_f32xN<T>(gamma + N * l, gv);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        xh[e] = (xh[e] - mu) * rs;
+        g[e] = d[e] * gv[e];
+        s1 += g[e];
+        s2 += g[e] * xh[e];
+        pg[e] += d[e] * xh[e];
+        pb[e] += d[e];
+      }
+    }
+    const float c1 = group_sum<LPR>(s1) / (float)width;
+    const float c2 = group_sum<LPR>(s2) / (float)width;
+    if (on) {
+      float o[N];
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] = rs * (g[e] - c1 - xh[e] * c2) + (dx_add ? add[e] : 0.f);
+      VN<T>::store(dx + row * lddx + N * l, o);
+      if (dx_drop) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const uint32_t h = mmfd_hash(seed, salt, (uint64_t)row * (uint64_t)width + N * l + e);
+          o[e] = (p > 0.f && h < thr) ? 0.f : o[e] * (p > 0.f ? keep : 1.f);
+        }
+        VN<T>::store(dx_drop + row * lddx + N * l, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    red[wave][0][lane * N + e] = pg[e];
+    red[wave][1][lane * N + e] = pb[e];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < width; col += 256) {  // col = chunk * N + e, chunk < LPR
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        sg += red[w][0][r * LPR * N + col];
+        sb += red[w][1][r * LPR * N + col];
+      }
+    part[((int64_t)blockIdx.x * 2 + 0) * width + col] = sg;
+    part[((int64_t)blockIdx.x * 2 + 1) * width + col] = sb;
+  }
+}
+
 }  // namespace
 
 extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
@@ -492,7 +571,22 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
   const bool v16 = width % epc == 0 && lddy % epc == 0 && ldx % epc == 0 && lddx % epc == 0 &&
                    (!dx_add || (ldadd % epc == 0 && al(dx_add))) && al(dy) && al(x) && al(dx) && al(gamma) &&
                    (!dx_drop || al(dx_drop));
-  if (v16) {
+  const int nch16 = (int)(width / epc);
+  if (v16 && nch16 <= 32) {
+    // narrow rows: RPW rows per wave, so a block covers 4 * RPW rows
+    const int rpb = nch16 <= 16 ? 16 : 8;
+    nblocks = (int)std::min<int64_t>((rows + rpb - 1) / rpb, 2048);
+    if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
+#define LNB(T, LPR) hipLaunchKernelGGL((ln_bwd16_narrow_kernel<T, LPR>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, \
+                                       (const T*)dy, lddy, (const T*)x, ldx, gamma, mean, rstd, (T*)dx, lddx,             \
+                                       (const T*)dx_add, ldadd, (T*)dx_drop, p, thr, seed, salt, (float*)workspace)
+    if (dtype == MMFD_BF16) {
+      if (nch16 <= 16) LNB(bf16, 16); else LNB(bf16, 32);
+    } else {
+      if (nch16 <= 16) LNB(float, 16); else LNB(float, 32);
+    }
+#undef LNB
+  } else if (v16) {
     if (dtype == MMFD_BF16)
       hipLaunchKernelGGL((ln_bwd16_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
                          (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd,
