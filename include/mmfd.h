@@ -131,6 +131,11 @@ typedef struct mmfd_attn_args {
   int64_t rel_bias_sb;             /* batch stride of rel_bias in floats (0 = shared by the batch) */
   int64_t rel_bias_mod;            /* > 0: batch row b reads bias row b % rel_bias_mod (Swinv2 windows:
                                       [nW][H][L][L] shift masks, batch = images x nW windows) */
+  const float* cos_logit_scale;    /* forward only, NULL = plain attention. Otherwise Swinv2 cosine
+                                      attention: q_h, k_h are L2-normalised (eps 1e-12) and q_h scaled
+                                      by exp(min(cos_logit_scale[h], cos_max_log)) while staged (bf16,
+                                      Lk <= 256, rel_bias required); replaces mmfd_swin_qk_norm */
+  float cos_max_log;
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);

@@ -33,6 +33,7 @@ struct AttnP {
   float* lse;
   const float* key_bias;
   const float* rel_bias; int64_t rb_sb, rb_mod;
+  const float* cos_ls; float cos_max_log;  // Swinv2 cosine attention (REL forward only)
   float p; uint32_t thr; float keep_scale;
   const uint64_t* seed; uint64_t salt;
   const void* dout; int64_t do_sb, do_st;
@@ -514,6 +515,55 @@ __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base,
   }
 }
 
+// K rows staged as k / max(|k|, 1e-12) (Swinv2 cosine attention): the NCH chunks of a row belong to
+// NCH consecutive lanes, so the row's sum of squares is a butterfly over those lanes
+template <int D, int NTH>
+__device__ __forceinline__ void stage_rows_cos(char* lds, const bf16* __restrict__ base, int64_t st, int64_t nrows,
+                                               int nrows_pad, int tid, int dreal) {
+  constexpr int NCH = AT<bf16, D>::NCH, EPC = AT<bf16, D>::EPC;
+  for (int c = tid; c < nrows_pad * NCH; c += NTH) {
+    const int r = c / NCH, ch = c % NCH;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nrows && ch * EPC < dreal) v = *reinterpret_cast<const uint4*>(base + (int64_t)r * st + ch * EPC);
+    const bf16x8 x = __builtin_bit_cast(bf16x8, v);
+    float f[EPC], ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) { f[e] = (float)x[e]; ss = fmaf(f[e], f[e], ss); }
+#pragma unroll
+    for (int o = 1; o < NCH; o <<= 1) ss += __shfl_xor(ss, o, 64);
+    const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    bf16x8 y;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) y[e] = (bf16)(f[e] * inv);
+    *reinterpret_cast<uint4*>(lds + row_off<bf16, D>(r, ch)) = __builtin_bit_cast(uint4, y);
+  }
+}
+
+// q fragments (load_row_regs layout: a row's chunks sit in lanes li, li+16, li+32, li+48) scaled to
+// q / max(|q|, 1e-12) * mult, rounded as the separate normalisation pass would
+template <int D>
+__device__ __forceinline__ void cos_norm_q(uint4* f, float mult) {
+  constexpr int KCH = AT<bf16, D>::KCH;
+  float ss = 0.f;
+  float v[KCH][8];
+#pragma unroll
+  for (int kc = 0; kc < KCH; ++kc) {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, f[kc]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[kc][e] = (float)x[e]; ss = fmaf(v[kc][e], v[kc][e], ss); }
+  }
+  ss += __shfl_xor(ss, 16, 64);
+  ss += __shfl_xor(ss, 32, 64);
+  const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+  for (int kc = 0; kc < KCH; ++kc) {
+    bf16x8 y;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = (bf16)((v[kc][e] * inv) * mult);
+    f[kc] = __builtin_bit_cast(uint4, y);
+  }
+}
+
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 
 // per-key additive bias in log2 units for the head's batch row: log2e * key_bias (clamped so a
@@ -548,7 +598,11 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   char* v_img = hbase + lk_pad * C::RB;
   float* kbias = reinterpret_cast<float*>(hbase + 2 * lk_pad * C::RB);
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
-  stage_all<T, D, false, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
+  const bool cosine = REL && p.cos_ls != nullptr;
+  if (cosine)
+    stage_rows_cos<D, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
+  else
+    stage_all<T, D, false, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
   stage_all<T, D, true, TPH>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, htid, p.D);
   stage_kbias<TPH>(kbias, p, b, lk_pad, htid);
   __syncthreads();
@@ -556,6 +610,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
+  const float qmult = cosine ? expf(fminf(p.cos_ls[h], p.cos_max_log)) : 1.f;
   const bool rel4 = p.rel_bias && (p.Lk & 3) == 0 && (reinterpret_cast<uintptr_t>(p.rel_bias) & 15) == 0 &&
                     (p.rb_sb & 3) == 0;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
@@ -568,6 +623,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
     for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
     load_row_regs<T, D>(qn, qb, p.q_st, q0 + WPH * 16 + li, p.Lq, lane, p.D);
+    if (cosine) cos_norm_q<D>(qf, qmult);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
@@ -874,6 +930,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
     MMFD_CHECK_ARG(a.dout && a.dq && a.dk && a.dv && a.delta, "attn_bwd: null pointer");
     MMFD_CHECK_ARG(al(a.dout, a.do_sb, a.do_st), "attn_bwd: dout alignment");
     MMFD_CHECK_ARG(a.d_rel_bias == nullptr, "attn_bwd: relative-bias gradient not supported");
+    MMFD_CHECK_ARG(a.cos_logit_scale == nullptr, "attn_bwd: cosine attention is inference-only");
   }
   p.B = a.B; p.H = a.H; p.Lq = a.Lq; p.Lk = a.Lk; p.scale = a.scale; p.D = (int)a.D;
   p.q = a.q; p.q_sb = a.q_sb; p.q_st = a.q_st;
@@ -882,6 +939,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.o = a.o; p.o_sb = a.o_sb; p.o_st = a.o_st;
   p.lse = a.lse; p.key_bias = a.key_bias; p.rel_bias = a.rel_bias; p.rb_sb = a.rel_bias ? a.rel_bias_sb : 0;
   p.rb_mod = a.rel_bias ? a.rel_bias_mod : 0;
+  p.cos_ls = a.cos_logit_scale; p.cos_max_log = a.cos_max_log;
   p.p = a.dropout_p > 0.f ? a.dropout_p : 0.f; p.thr = mmfd_drop_threshold(p.p);
   p.keep_scale = 1.0f / (1.0f - p.p); p.seed = a.seed; p.salt = a.salt;
   p.dout = a.dout; p.do_sb = a.do_sb; p.do_st = a.do_st;
@@ -984,6 +1042,8 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   // batch-1 pair at L = 512 runs faster on the 64-query-block streaming kernel)
   const bool v2 = a->dtype == MMFD_BF16 && (p.Lk <= V2_LMAX || (p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) &&
                   !getenv("MMFD_ATTN_V1");
+  MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && a->rel_bias),
+                 "attn_fwd: cosine attention needs the bf16 resident-K/V kernel (Lk <= 256) and a rel_bias");
   if (v2) { if (a->D > 32) launch_fwd_v2<64>(p, s); else launch_fwd_v2<32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }

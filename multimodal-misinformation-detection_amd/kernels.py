@@ -77,6 +77,8 @@ class AttnArgs(ctypes.Structure):
         ("accumulate_dkv", ctypes.c_int),
         ("rel_bias_sb", ctypes.c_int64),
         ("rel_bias_mod", ctypes.c_int64),
+        ("cos_logit_scale", ctypes.c_void_p),
+        ("cos_max_log", ctypes.c_float),
     ]
 
 
@@ -382,8 +384,10 @@ def _head_view(t, H, D):
     return t.data_ptr(), t.stride(0), t.stride(1)
 
 
-def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, dropout_p=0.0, seed=None, salt=0):
+def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, dropout_p=0.0, seed=None, salt=0,
+             cos_logit_scale=None, cos_max_log=0.0):
     """q: [B, Lq, H*D], k/v: [B, Lk, H*D] (views into fused QKV buffers are fine).
+    cos_logit_scale (fp32 [H], bf16 only): Swinv2 cosine attention, q/k normalised in the kernel.
     Returns (o [B, Lq, H*D], lse [B, H, Lq] fp32)."""
     _require_cuda(q, k, v)
     B, Lq, HD = q.shape
@@ -406,6 +410,11 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
     a.dropout_p = float(dropout_p)
     a.seed = seed.t.data_ptr() if seed is not None else None
     a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    if cos_logit_scale is not None:
+        if cos_logit_scale.dtype != torch.float32 or not cos_logit_scale.is_contiguous():
+            raise ValueError("cos_logit_scale must be a contiguous fp32 tensor of H values")
+        a.cos_logit_scale = cos_logit_scale.data_ptr()
+        a.cos_max_log = float(cos_max_log)
     _check(lib().mmfd_attn_fwd(ctypes.byref(a), _stream()), "mmfd_attn_fwd")
     return out, lse
 

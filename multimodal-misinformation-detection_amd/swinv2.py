@@ -20,8 +20,9 @@ block's (shifted) window order, so the per-token GEMMs / LayerNorms run on the p
 they are and the only data movement is ONE `mmfd_row_gather` per block that composes the previous
 block's order with the next one (roll + window_partition + window_reverse + roll back in a single
 pass), and one for each patch merge (which reads the 2x2 neighbours straight out of window order).
-QKV is one packed GEMM; the cosine normalisation and the per-head logit scale are one in-place pass
-over the packed rows; the continuous position bias (+ shift mask) is computed once per block into a
+QKV is one packed GEMM; the cosine normalisation and the per-head logit scale happen inside the
+attention kernel while it stages K and the query fragments (bf16; the fp32 parity mode uses one
+in-place pass over the packed rows, `mmfd_swin_qk_norm`); the continuous position bias (+ shift mask) is computed once per block into a
 [nW, H, 64, 64] fp32 table that the flash-attention kernel reads with a batch modulus
 (`rel_bias_mod`): windows are batch-major per image, so window w of every image shares bias row w.
 Inference only (the reference freezes its encoders, train.py:335-340, and the pre-embedding pass
@@ -283,7 +284,9 @@ def swinv2_forward(model: Swinv2Model, ctx: Bk.StepCtx, geo: _Geo, pixel_values)
 def _swin_block(ctx, geo, x, pre, B, R, dim, H, d, ws, shift, nW, L, eps, cfg):
     s = pre + ".attention.self"
     qkv = Bk.linear_packed(ctx, x, [s + ".query", s + ".key", s + ".value"])   # [N, 3*dim]
-    K.swin_qk_norm(qkv, H, d, ctx.P[s + ".logit_scale"], math.log(1.0 / 0.01))
+    fused = ctx.dt == torch.bfloat16          # bf16: the attention kernel normalises q / k while staging
+    if not fused:
+        K.swin_qk_norm(qkv, H, d, ctx.P[s + ".logit_scale"], math.log(1.0 / 0.01))
     stage = int(pre.split(".")[2])
     pws = cfg.pretrained_window_sizes[stage]
     coords, rpi = geo.get(("cpb", ws, pws), lambda: tuple(t.to(geo.dev) for t in coords_table_and_index(ws, pws)))
@@ -297,7 +300,9 @@ def _swin_block(ctx, geo, x, pre, B, R, dim, H, d, ws, shift, nW, L, eps, cfg):
                        lambda: K.swin_bias(K.swin_cpb(coords, *[ctx.P[n] for n in cpb]), rpi, L, mask))
     q3 = qkv.view(B * nW, L, 3 * dim)
     o, _ = K.attn_fwd(q3[..., :dim], q3[..., dim:2 * dim], q3[..., 2 * dim:], H, scale=1.0,
-                      rel_bias=bias if shift > 0 else bias.view(H, L, L))
+                      rel_bias=bias if shift > 0 else bias.view(H, L, L),
+                      cos_logit_scale=ctx.P[s + ".logit_scale"].view(-1) if fused else None,
+                      cos_max_log=math.log(1.0 / 0.01))
     y, _ = Bk.linear(ctx, Bk.as2d(o), pre + ".attention.output.dense")
     h = K.layernorm_fwd_res(y, ctx.P[pre + ".layernorm_before.weight"], ctx.P[pre + ".layernorm_before.bias"], eps,
                             res=x)

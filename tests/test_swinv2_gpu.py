@@ -101,6 +101,26 @@ def test_attention_bias_modulus_matches_per_window_bias():
     assert torch.equal(o1, o2)
 
 
+@pytest.mark.parametrize("nW,L", [(4, 64), (1, 64), (2, 16)])
+def test_attention_fused_cosine_matches_separate_pass(nW, L):
+    """bf16 attention with cos_logit_scale (q/k normalised while staged) == mmfd_swin_qk_norm followed
+    by plain attention, on the same bf16 inputs"""
+    from mmfd import kernels as K
+    Bi, H, d = 3, 4, 32
+    torch.manual_seed(L + nW)
+    qkv = (torch.randn(Bi * nW * L, 3 * H * d, device="cuda") * 2).bfloat16()
+    qkv[7, :d] = 0
+    ls = torch.tensor([0.5, 2.3, 5.0, -1.0], device="cuda")
+    bias = torch.randn(nW, H, L, L, device="cuda")
+    sep = K.swin_qk_norm(qkv.clone(), H, d, ls, math.log(100.0)).view(Bi * nW, L, 3 * H * d)
+    o1, _ = K.attn_fwd(sep[..., :H * d], sep[..., H * d:2 * H * d], sep[..., 2 * H * d:], H, scale=1.0, rel_bias=bias)
+    q3 = qkv.view(Bi * nW, L, 3 * H * d)
+    o2, _ = K.attn_fwd(q3[..., :H * d], q3[..., H * d:2 * H * d], q3[..., 2 * H * d:], H, scale=1.0, rel_bias=bias,
+                       cos_logit_scale=ls, cos_max_log=math.log(100.0))
+    torch.cuda.synchronize()
+    assert (o1.float() - o2.float()).abs().max().item() < 2e-2
+
+
 def _cfg(**kw):
     from mmfd.swinv2 import Swinv2Config
     return Swinv2Config(**kw)
