@@ -114,3 +114,31 @@ def test_deberta_host_buckets_and_names():
                share_att_key=True, pos_att_type=["p2c", "c2p"], position_biased_input=False, type_vocab_size=0,
                **kw)).state_dict()
     assert {k: tuple(v.shape) for k, v in ours.items()} == {k: tuple(v.shape) for k, v in hf.items()}
+
+
+def test_stepctx_derived_cache_tracks_weight_versions():
+    """weight-derived tensors (packed biases, Swinv2 position-bias tables) persist across calls of a
+    frozen encoder and are rebuilt after an in-place weight change; training contexts never cache"""
+    import torch
+    from mmfd import blocks as Bk
+
+    w = torch.ones(4)
+    store = {}
+    calls = []
+
+    def make():
+        calls.append(1)
+        return w * 2
+
+    for _ in range(3):
+        ctx = Bk.StepCtx({"w": w}, torch.float32, shadows=store)
+        ctx.cache_derived = True
+        t = ctx.derived("k", ["w"], make)
+    assert len(calls) == 1 and torch.equal(t, torch.full((4,), 2.0))
+    w.add_(1.0)
+    ctx = Bk.StepCtx({"w": w}, torch.float32, shadows=store)
+    ctx.cache_derived = True
+    assert torch.equal(ctx.derived("k", ["w"], make), torch.full((4,), 4.0)) and len(calls) == 2
+    ctx = Bk.StepCtx({"w": w}, torch.float32, shadows=store)      # cache_derived off (training)
+    ctx.derived("k", ["w"], make)
+    assert len(calls) == 3
