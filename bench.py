@@ -3,8 +3,13 @@ bert-base-uncased + ViT-B/16 + fusion head, forward + backward + AdamW, bs=256 p
 224x224 images, synthetic data already resident in HBM), data parallel over N GPUs (one process per
 GPU, RCCL gradient all-reduce). Prints ONE JSON line on rank 0.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision bf16|fp32]
-                  [--mode finetune|frozen] [--no-cpu-baseline] [--workload train|forward|extract|retrieve|preprocess|latency|preembed|preembed_image]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--precision fp32|bf16]
+                  [--mode finetune|frozen] [--no-cpu-baseline] [--no-bf16]
+                  [--workload train|forward|extract|retrieve|preprocess|latency|preembed|preembed_image]
+
+The train headline is fp32 (the reference's arithmetic; logits within 1e-3 of the CPU oracle); the
+same step in bf16 (bf16 MFMA operands, fp32 accumulation and master weights) is reported beside it
+under "bf16". `--gpus N` outside a torch.distributed launcher starts N ranks itself.
 """
 import argparse
 import json
@@ -23,28 +28,109 @@ GFLOP_PER_PAIR = {"finetune": 351.18, "frozen": 121.11}  # BASELINE.md §3 (Flop
 PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(steps=2, batch=4):
-    """The oracle's CPU restatement of the same step, timed on this host (bounded sample)."""
+def host_cores():
+    """Threads for the CPU baseline: every core of the affinity mask, capped by the
+    cgroup CPU quota when one is set (a GPU box grants a 16-CPU share of a larger machine; more
+    threads than the quota only oversubscribe it)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def log(msg):
+    """progress on stderr (the JSON line on stdout stays the only stdout output)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _timed(fn, steps):
+    fn()  # warmup
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    return (time.perf_counter() - t0) / steps
+
+
+def cpu_baseline(dev, steps=3, batch=4):
+    """The oracle's CPU restatement (oracle/, validated against the reference's own fixtures) timed
+    on this host with every core of the affinity mask: 1 warmup + `steps` timed steps
+    of configs 1, 2 and 3 at bs=4. Config 2's oracle logits also give the measured full-size
+    deviation of the HIP path's fp32 and bf16 logits (same weights and inputs)."""
+    from oracle import encoders as OE
+    from oracle import fusion_head as OF
     from oracle.fusion_head import init_params_like_reference
     from oracle.train_step import BERT_BASE, VIT_B16, OracleTrainer, bert_names, vit_names
-    from mmfd.dataset import synthetic_batch
+    from mmfd.dataset import LABEL_TABLE, synthetic_batch
     from mmfd.model import MisinformationDetectionModel
+    from mmfd.train import build_flagship
 
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = host_cores()
     torch.set_num_threads(cores)
+    # config 3: full fine-tune step (the headline workload)
     head_names = [(k, list(v.shape)) for k, v in MisinformationDetectionModel(768, 768).state_dict().items()]
     tr = OracleTrainer(init_params_like_reference(bert_names(BERT_BASE), 1),
                        init_params_like_reference(vit_names(VIT_B16), 2),
                        init_params_like_reference(head_names, 3))
     b = synthetic_batch(batch, device="cpu", seed=7)
-    tr.step(b)  # warmup
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.step(b)
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": round(batch / dt, 4), "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"oracle CPU restatement (fp32 torch CPU) of the same full fine-tune step at bs={batch}, "
-                      f"1 warmup + {steps} timed steps, {dt:.2f} s/step"}
+    log(f"cpu baseline: config 3 on {cores} threads")
+    dt3 = _timed(lambda: tr.step(b), steps)
+    del tr
+    # config 2: dual encoder + head forward (eval), with the GPU deviation on the same inputs
+    g2 = build_flagship(dev, "fp32", seed=3)
+    sd = lambda m: {k: v.detach().float().cpu() for k, v in m.state_dict().items()}  # noqa: E731
+    bp, vp, hp = sd(g2.text_encoder), sd(g2.image_encoder), sd(g2.head)
+    b2 = synthetic_batch(batch, device="cpu", seed=17, ragged=True)
+
+    def fwd2():
+        with torch.no_grad():
+            T = OE.bert_forward(bp, b2["input_ids"], b2["attention_mask"], None, num_layers=12, num_heads=12)
+            I = OE.vit_forward(vp, b2["pixel_values"], num_layers=12, num_heads=12, patch=16)
+            return OF.model_forward(hp, T[:batch], I[:batch], T[batch:], I[batch:], num_heads=8)
+
+    log("cpu baseline: config 2")
+    dt2 = _timed(fwd2, steps)
+    want = torch.stack([y for pr in fwd2() for y in pr])
+    dev_err = {}
+    for prec in ("fp32", "bf16"):
+        for m in (g2.text_encoder, g2.image_encoder, g2.head):
+            m.set_precision(prec)
+        got = g2.predict({k: v.to(dev) for k, v in b2.items()})
+        got = torch.stack([y for pr in got for y in pr]).float().cpu()
+        dev_err[prec] = float((got - want).abs().max())
+    del g2
+    # config 1: reference-default head training on pre-embedded inputs (train.py:343-356 dims)
+    P1 = OF.xavier_like_reference([(k, list(v.shape)) for k, v in
+                                   MisinformationDetectionModel(384, 1024).state_dict().items()], 5)
+    P1 = {k: v.requires_grad_(True) for k, v in P1.items()}
+    opt = torch.optim.AdamW(list(P1.values()), lr=1e-4)
+    g = torch.Generator().manual_seed(9)
+    Xt, Et = torch.randn(batch, 512, 384, generator=g), torch.randn(batch, 512, 384, generator=g)
+    Xi, Ei = torch.randn(batch, 64, 1024, generator=g), torch.randn(batch, 64, 1024, generator=g)
+    lab = LABEL_TABLE[torch.randint(0, 5, (batch,), generator=g)]
+
+    def step1():
+        opt.zero_grad(set_to_none=True)
+        tot, _ = OF.path_loss(OF.model_forward(P1, Xt, Xi, Et, Ei, num_heads=8), lab)
+        tot.backward()
+        opt.step()
+
+    log("cpu baseline: config 1")
+    dt1 = _timed(step1, steps)
+    out = {"value": round(batch / dt3, 4), "unit": "pairs/s", "cores": cores, "kind": "port",
+           "sample": f"oracle/ CPU restatement (fp32 torch, {cores} threads = the affinity mask), bs={batch}, "
+                     f"1 warmup + {steps} timed steps per config; value = config 3 (full fine-tune step, "
+                     f"{dt3:.2f} s/step)",
+           "configs": {"config1_head_train_384_1024_L512_64": round(batch / dt1, 3),
+                       "config2_forward_bert_vit_head": round(batch / dt2, 3),
+                       "config3_finetune_step": round(batch / dt3, 4)}}
+    parity = {"config2_fp32_max_abs_logit_err": dev_err["fp32"], "config2_bf16_max_abs_logit_err": dev_err["bf16"],
+              "inputs": f"{batch} full-size pairs (ragged masks), same weights, eval"}
+    return out, parity
 
 
 def pmc_traffic(kernel):
@@ -507,29 +593,30 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default=None,
+                    help="train: fp32 (default; the reference's arithmetic, bf16 reported beside it); other workloads: bf16")
     ap.add_argument("--mode", choices=["finetune", "frozen"], default="finetune")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["train", "forward", "extract", "retrieve", "preprocess", "latency",
                                                   "preembed", "preembed_image"],
                     default="train")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the secondary bf16 leg of the fp32 headline")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dp = None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-        from mmfd.dp import GradAllReduce
-        dp = GradAllReduce()
+    if args.precision is None:
+        args.precision = "fp32" if args.workload == "train" else "bf16"
 
-    import mmfd
+    import mmfd  # noqa: F401
     from mmfd import kernels as K
-    from mmfd.dataset import synthetic_batch
-    from mmfd.train import build_flagship
 
     K.load()
     if args.workload == "extract":
@@ -550,7 +637,56 @@ def main():
         if args.batch == 256:
             args.batch = 64
         return preembed_main(args, dev, world, rank)
-    tr = build_flagship(dev, args.precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42 + rank)
+    res = train_leg(args, dev, world, rank, args.precision)
+    log(f"{args.precision} leg: {res['pairs']:.1f} pairs/s")
+    sec = None
+    if args.precision == "fp32" and not args.no_bf16:
+        torch.cuda.empty_cache()
+        sec = train_leg(args, dev, world, rank, "bf16")
+        log(f"bf16 leg: {sec['pairs']:.1f} pairs/s")
+    if rank == 0:
+        peak = PEAK_TFLOPS[args.precision]
+        out = {
+            "metric": METRIC, "value": round(res["pairs"], 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.precision, "data": "synthetic (Factify-shaped pairs, random-init weights)",
+            "config": {"workload": ("full fine-tune " if args.mode == "finetune" else "frozen-encoder ") +
+                       "bert-base-uncased + ViT-B/16 + fusion head (768/768, E=256, H=8), fwd+bwd+AdamW",
+                       "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
+                       "parallelism": f"dp{world}"},
+            "roofline": res["roofline"],
+            "step_tflops_per_gpu": round(res["step_tflops"], 1),
+            "step_mfma_frac": round(res["step_tflops"] / peak, 4),
+            "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
+            "final_loss": res["loss"],
+        }
+        if sec is not None:
+            out["bf16"] = {"value": round(sec["pairs"], 2), "unit": "pairs/s", "ms_per_step": round(sec["ms"], 3),
+                           "step_tflops_per_gpu": round(sec["step_tflops"], 1),
+                           "step_mfma_frac": round(sec["step_tflops"] / PEAK_TFLOPS["bf16"], 4),
+                           "roofline": sec["roofline"], "final_loss": sec["loss"],
+                           "note": "secondary: bf16 MFMA operands, fp32 accumulation / master weights / optimizer"}
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"], out["parity"] = cpu_baseline(dev)
+            except Exception as e:  # the baseline must never hide the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def train_leg(args, dev, world, rank, precision):
+    """`--warmup` untimed + `--steps` timed training steps of one precision; returns the numbers."""
+    from mmfd import kernels as K
+    from mmfd.dataset import synthetic_batch
+    from mmfd.train import build_flagship
+
+    dp = None
+    if world > 1:
+        from mmfd.dp import GradAllReduce
+        dp = GradAllReduce()
+    tr = build_flagship(dev, precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42, rank=rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 
     for _ in range(args.warmup):
@@ -578,43 +714,35 @@ def main():
     loss_val = loss[0].item()
 
     prof = probe.summary()
-    dom = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
-    dom_name, d = dom
+    dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.precision]
+    peak = PEAK_TFLOPS[precision]
     gemm_ms = sum(v["ms"] for v in prof.values()) / args.steps
     gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
-
     traffic, traffic_src = pmc_traffic(dom_name)
-    if rank == 0:
-        step_tflops = pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3
-        out = {
-            "metric": METRIC, "value": round(pairs, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": args.precision, "data": "synthetic (Factify-shaped pairs, random-init weights)",
-            "config": {"workload": ("full fine-tune " if args.mode == "finetune" else "frozen-encoder ") +
-                       "bert-base-uncased + ViT-B/16 + fusion head (768/768, E=256, H=8), fwd+bwd+AdamW",
-                       "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
-                       "parallelism": f"dp{world}"},
+    del tr, batch
+    return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2),
+            "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
             "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "traffic_source": traffic_src,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "launches_per_step": d["launches"] // args.steps,
                          "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
-                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])},
-            "step_tflops_per_gpu": round(step_tflops, 1),
-            "step_mfma_frac": round(step_tflops / peak, 4),
-            "gemm_ms_per_step": round(gemm_ms, 2), "gemm_tflops_all_shapes": round(gemm_tf, 1),
-            "final_loss": round(loss_val, 4),
-        }
-        if not args.no_cpu_baseline and world == 1:
-            try:
-                out["cpu_baseline"] = cpu_baseline()
-            except Exception as e:  # the baseline must never hide the GPU number
-                out["cpu_baseline"] = {"error": repr(e)}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])}}
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a torch.distributed launcher: start one rank per GPU via
+    torch.distributed.run as a CHILD process (this process has not touched the GPU) and exit with
+    its status. Under the driver's own `torch.distributed.run` launch WORLD_SIZE is already set."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 if __name__ == "__main__":

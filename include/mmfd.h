@@ -174,15 +174,19 @@ int mmfd_seq_mean_bwd(int dtype, int64_t B, int64_t L, int64_t D, const void* do
                       void* dx, mmfd_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------- */
-/* Summed per-path cross entropy (train.py:165-169: sum_i CrossEntropyLoss(y_i, labels[:, i])).  */
-/* logits: HOST array of n_paths device pointers, each [B][C] fp32; labels int64 (device)      */
-/* [B][label_ld] with path i in column i. loss[0] = total, loss[1+i] = path i (mean over B).     */
+/* Summed per-path cross entropy (train.py:165-169: sum over PRESENT paths idx of                */
+/* CrossEntropyLoss(y_idx, labels[:, idx]); absent paths (None outputs) contribute nothing).     */
+/* logits: HOST array of n_paths device pointers, each [B][C] fp32; path_cols: HOST array of    */
+/* n_paths label columns (the reference's path index idx, train.py:165; NULL = 0..n_paths-1);   */
+/* labels int64 (device) [B][label_ld]. loss (device, n_slots >= 1 + max column) receives       */
+/* loss[0] = total, loss[1+col] = that path's mean loss and 0 for columns with no present path.  */
 /* dlogits (optional host array of n_paths device pointers) receive d(total)/d(logits) *        */
 /* (*dloss_scale or 1), dloss_scale being a device scalar (NULL = 1).                            */
 /* ------------------------------------------------------------------------------------------- */
 int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits,
-                      const int64_t* labels, int64_t label_ld, float* loss, float* const* dlogits,
-                      const float* dloss_scale, mmfd_stream_t stream);
+                      const int* path_cols, const int64_t* labels, int64_t label_ld, float* loss,
+                      int n_slots, float* const* dlogits, const float* dloss_scale,
+                      mmfd_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------- */
 /* BERT embeddings (HF BertEmbeddings: word + position + token_type, LayerNorm, dropout).       */

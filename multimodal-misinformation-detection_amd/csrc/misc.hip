@@ -81,11 +81,12 @@ __global__ void seq_mean_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __
 struct XentPtrs {
   const float* logits[4];
   float* dlogits[4];
+  int col[4];  // label column (= the reference's path index, train.py:165) of each present path
   int has_grad;
 };
 
 __global__ void xent_kernel(int n_paths, int64_t B, int64_t C, XentPtrs ptrs, const int64_t* __restrict__ labels,
-                            int64_t label_ld, float* __restrict__ loss, const float* __restrict__ dscale) {
+                            int64_t label_ld, float* __restrict__ loss, int n_slots, const float* __restrict__ dscale) {
   __shared__ float red[4][256];
   const float sc = dscale ? *dscale : 1.0f;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
@@ -98,7 +99,7 @@ __global__ void xent_kernel(int n_paths, int64_t B, int64_t C, XentPtrs ptrs, co
     float se = 0.f;
     for (int64_t c = 0; c < C; ++c) se += expf(z[c] - mx);
     const float lse = mx + logf(se);
-    const int64_t y = labels[b * label_ld + path];
+    const int64_t y = labels[b * label_ld + ptrs.col[path]];
     part[path] += lse - z[y];
     if (ptrs.has_grad) {
       float* dz = ptrs.dlogits[path] + b * C;
@@ -113,10 +114,11 @@ __global__ void xent_kernel(int n_paths, int64_t B, int64_t C, XentPtrs ptrs, co
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    for (int s = 1; s < n_slots; ++s) loss[s] = 0.f;
     float tot = 0.f;
     for (int p = 0; p < n_paths; ++p) {
       const float lp = red[p][0] / (float)B;
-      loss[1 + p] = lp;
+      loss[1 + ptrs.col[p]] = lp;
       tot += lp;
     }
     loss[0] = tot;
@@ -382,19 +384,22 @@ extern "C" int mmfd_seq_mean_bwd(int dtype, int64_t B, int64_t L, int64_t D, con
   return 0;
 }
 
-extern "C" int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits, const int64_t* labels,
-                                 int64_t label_ld, float* loss, float* const* dlogits, const float* dloss_scale,
-                                 mmfd_stream_t stream) {
+extern "C" int mmfd_xent_fwd_bwd(int n_paths, int64_t B, int64_t C, const float* const* logits, const int* path_cols,
+                                 const int64_t* labels, int64_t label_ld, float* loss, int n_slots,
+                                 float* const* dlogits, const float* dloss_scale, mmfd_stream_t stream) {
   MMFD_CHECK_ARG(n_paths >= 1 && n_paths <= 4, "xent: 1..4 paths");
   MMFD_CHECK_ARG(B > 0 && C > 0 && logits, "xent: bad shape");
   XentPtrs ptrs = {};
   for (int i = 0; i < n_paths; ++i) {
     ptrs.logits[i] = logits[i];
     ptrs.dlogits[i] = dlogits ? dlogits[i] : nullptr;
+    ptrs.col[i] = path_cols ? path_cols[i] : i;
+    MMFD_CHECK_ARG(ptrs.col[i] >= 0 && ptrs.col[i] < label_ld && 1 + ptrs.col[i] < n_slots,
+                   "xent: label column outside labels / loss slots");
   }
   ptrs.has_grad = dlogits != nullptr;
   hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_paths, B, C, ptrs, labels, label_ld, loss,
-                     dloss_scale);
+                     n_slots, dloss_scale);
   MMFD_CHECK_LAUNCH("xent");
   return 0;
 }

@@ -75,6 +75,34 @@ class GradAllReduce:
                 off += n
         self.begin()
 
+    def broadcast_params(self, params, src=0):
+        """Make every rank start from rank `src`'s parameters (called once when a trainer is built:
+        ranks may have initialised their replicas from different seeds). Parameters are flattened
+        into bucket-sized fp32 buffers, one broadcast per bucket; the copies back are plain
+        in-place writes, so bf16 weight shadows built later see the broadcast values."""
+        if not self._active():
+            return
+        params = [p for p in params]
+        i = 0
+        while i < len(params):
+            j, n = i, 0
+            while j < len(params) and (j == i or n + params[j].numel() <= self.bucket_elems):
+                n += params[j].numel()
+                j += 1
+            group = params[i:j]
+            buf = torch.empty(n, device=group[0].device, dtype=torch.float32)
+            off = 0
+            with torch.no_grad():
+                for p in group:
+                    buf[off:off + p.numel()].copy_(p.detach().reshape(-1))
+                    off += p.numel()
+                dist.broadcast(buf, src=src, group=self.group)
+                off = 0
+                for p in group:
+                    p.detach().copy_(buf[off:off + p.numel()].view(p.shape))
+                    off += p.numel()
+            i = j
+
     def allreduce_grads(self, params):
         """non-overlapped form: average every .grad of `params`"""
         self.begin()

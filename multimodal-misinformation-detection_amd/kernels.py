@@ -107,7 +107,7 @@ SIGNATURES = {
                                 _VP, _VP, _F, _VP, _F, _VP, _U64, _VP, _I64, _VP]),
     "mmfd_seq_mean_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _I64, _VP]),
     "mmfd_seq_mean_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _I64, _VP, _VP]),
-    "mmfd_xent_fwd_bwd": (_I, [_I, _I64, _I64, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
+    "mmfd_xent_fwd_bwd": (_I, [_I, _I64, _I64, _VP, _VP, _VP, _I64, _VP, _I, _VP, _VP, _VP]),
     "mmfd_embed_ln_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
                                _F, _VP, _U64, _VP]),
     "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
@@ -569,20 +569,30 @@ def seq_mean_bwd(dout, L, dx=None):
     return dx
 
 
-def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None):
-    """logits: list of [B, C] fp32 tensors (paths), labels: int64 [B, n_paths (or more)].
-    Returns (loss [1 + n_paths] fp32 device tensor, list of dlogits or None)."""
+def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None, cols=None, n_slots=None):
+    """logits: list of [B, C] fp32 tensors (present paths), labels: int64 [B, n_cols] (or [B]);
+    cols: label column of each path (the reference's path index, train.py:165; default 0..n-1).
+    Returns (loss [n_slots] fp32 device tensor: total, then one slot per label column (0 for
+    columns without a present path), list of dlogits or None)."""
     n = len(logits)
     B, C = logits[0].shape
     dev = logits[0].device
+    cols = list(range(n)) if cols is None else [int(c) for c in cols]
+    if len(cols) != n:
+        raise ValueError("xent: one label column per path")
+    n_slots = n_slots or 1 + max(cols) + 1
     logits = [l.contiguous().float() for l in logits]
     labels = labels.contiguous()
-    loss = torch.empty(1 + n, device=dev, dtype=torch.float32)
+    ld = labels.stride(0) if labels.dim() > 1 else 1
+    if max(cols) >= (labels.shape[1] if labels.dim() > 1 else 1):
+        raise ValueError(f"xent: label column {max(cols)} outside labels {tuple(labels.shape)}")
+    loss = torch.empty(n_slots, device=dev, dtype=torch.float32)
     lp = (ctypes.c_void_p * n)(*[l.data_ptr() for l in logits])
+    cp = (ctypes.c_int * n)(*cols)
     dl = [torch.empty_like(l) for l in logits] if want_grad else None
     dp = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dl]) if want_grad else None
-    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp, _ptr(labels), labels.stride(0), _ptr(loss), dp, _ptr(dloss_scale),
-                                   _stream()), "mmfd_xent_fwd_bwd")
+    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp, cp, _ptr(labels), ld, _ptr(loss), int(n_slots), dp,
+                                   _ptr(dloss_scale), _stream()), "mmfd_xent_fwd_bwd")
     return loss, dl
 
 

@@ -14,6 +14,27 @@ import torch
 from . import kernels as K
 
 
+def _adopt_state(st, p):
+    """State loaded from a checkpoint (torch.optim.AdamW's `optimizer_state_dict`, or an mmfd one
+    loaded with map_location='cpu') may hold CPU tensors, a python-number / int step or
+    non-contiguous moments: the kernel reads raw device pointers, so move every entry onto the
+    parameter's device as contiguous fp32 (torch keeps a non-capturable 'step' on the CPU)."""
+    step = st.get("step", 0)
+    if not torch.is_tensor(step):
+        step = torch.tensor(float(step))
+    if step.device != p.device or step.dtype != torch.float32 or step.dim() != 0:
+        st["step"] = step.detach().reshape(()).to(device=p.device, dtype=torch.float32)
+    for k in ("exp_avg", "exp_avg_sq"):
+        t = st.get(k)
+        if t is None:
+            st[k] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            continue
+        if tuple(t.shape) != tuple(p.shape):
+            raise ValueError(f"AdamW state '{k}' has shape {tuple(t.shape)}, parameter {tuple(p.shape)}")
+        if t.device != p.device or t.dtype != torch.float32 or not t.is_contiguous():
+            st[k] = t.detach().to(device=p.device, dtype=torch.float32).contiguous()
+
+
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
@@ -62,8 +83,10 @@ class AdamW(torch.optim.Optimizer):
                 st = self.state[p]
                 if not st:
                     st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                else:
+                    _adopt_state(st, p)
                 entries.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step"]))
             if not entries:
                 continue

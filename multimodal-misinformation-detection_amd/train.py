@@ -28,11 +28,14 @@ PATHS = ("text_text", "text_image", "image_text", "image_image")
 
 
 class _XentFn(torch.autograd.Function):
-    """Summed per-path cross entropy (train.py:165-169) -> [total, path_0..path_3] (fp32, device)."""
+    """Summed per-path cross entropy (train.py:160-169) -> [total, text_text, text_image,
+    image_text, image_image] (fp32, device; 0 for an absent path). Path idx is trained on
+    labels[:, idx] whatever the other paths are (train.py:165)."""
 
     @staticmethod
-    def forward(ctx, labels, *logits):
-        loss, _ = K.xent_fwd_bwd(list(logits), labels, want_grad=False)
+    def forward(ctx, labels, cols, *logits):
+        loss, _ = K.xent_fwd_bwd(list(logits), labels, want_grad=False, cols=cols, n_slots=1 + len(PATHS))
+        ctx.cols = cols
         ctx.save_for_backward(labels, *logits)
         return loss
 
@@ -40,14 +43,24 @@ class _XentFn(torch.autograd.Function):
     def backward(ctx, g):
         labels, *logits = ctx.saved_tensors
         scale = g[:1].contiguous()  # d total; the per-path entries are for logging only
-        _, dl = K.xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=scale)
-        return (None, *dl)
+        _, dl = K.xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=scale, cols=ctx.cols,
+                               n_slots=1 + len(PATHS))
+        return (None, None, *dl)
 
 
 def path_losses(outputs, labels):
+    """outputs: ((y_tt, y_ti), (y_it, y_ii)) with None for absent paths (model.py:426-468)."""
     (ytt, yti), (yit, yii) = outputs
-    ys = [y for y in (ytt, yti, yit, yii) if y is not None]
-    return _XentFn.apply(labels, *ys)
+    present = [(i, y) for i, y in enumerate((ytt, yti, yit, yii)) if y is not None]
+    if not present:
+        raise ValueError("path_losses: every path output is None")
+    return _XentFn.apply(labels, tuple(i for i, _ in present), *[y for _, y in present])
+
+
+def category_loss(pred, labels):
+    """CrossEntropyLoss(pred, category index) of the single-output heads (factify=True 5-way,
+    eval_factify.py:114-139; text_only) -> [total, loss, 0, 0, 0] like path_losses."""
+    return _XentFn.apply(labels.reshape(-1), (0,), pred)
 
 
 class FusionTrainer:
@@ -70,7 +83,10 @@ class FusionTrainer:
         self.params = params
         self.optimizer = AdamW(params, lr=lr)
         self.dp = dp
-        if dp is not None:  # overlap the gradient all-reduce with the backward pass
+        if dp is not None:
+            # every replica starts from rank 0's weights (frozen encoders included: all ranks must
+            # compute the same function), then the gradient all-reduce overlaps the backward pass
+            dp.broadcast_params([p for m in (text_encoder, image_encoder, head) for p in m.parameters()])
             for m in ((head,) if freeze_encoders else (text_encoder, image_encoder, head)):
                 m._grad_ready = dp.hook_for(m)
 
@@ -111,15 +127,17 @@ class FusionTrainer:
 
 
 def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders=False, lr=1e-4, dp=None,
-                   seed=42):
-    """bert-base-uncased + ViT-B/16 + the fusion head at 768/768 (BASELINE configs 2-4), random init."""
+                   seed=42, rank=0):
+    """bert-base-uncased + ViT-B/16 + the fusion head at 768/768 (BASELINE configs 2-4), random init
+    from `seed` (the same on every rank; with `dp` rank 0's weights are broadcast anyway); the
+    dropout streams are offset per rank so replicas draw independent masks."""
     torch.manual_seed(seed)
     text = BertModel(BertConfig()).to(device)
     image = ViTModel(ViTConfig()).to(device)
     head = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768, embed_dim=256, num_heads=8,
                                         dropout=dropout, hidden_dim=64, num_classes=3).to(device)
-    text.manual_seed(seed)
-    head.manual_seed(seed + 1)
+    text.manual_seed(seed + 7919 * rank)
+    head.manual_seed(seed + 1 + 7919 * rank)
     return FusionTrainer(text, image, head, lr=lr, freeze_encoders=freeze_encoders, precision=precision, dp=dp)
 
 

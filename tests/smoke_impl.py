@@ -19,6 +19,9 @@ from oracle.train_step import OracleTrainer
 
 TINY = dict(D=64, layers=2, heads=4, inter=128, vocab=120, seq=16, img=32, patch=8, embed=32, head_heads=4,
             hidden=16)
+# BASELINE config 3 at full size: bert-base-uncased + ViT-B/16 + the fusion head (768/768, E=256, H=8)
+FULL = dict(D=768, layers=12, heads=12, inter=3072, vocab=30522, seq=128, img=224, patch=16, embed=256, head_heads=8,
+            hidden=64)
 
 
 def tiny_batch(B, cfg=TINY, seed=0, ragged=True):
@@ -37,7 +40,8 @@ def build_pair(precision="fp32", dropout=0.1, cfg=TINY, seed=5, lr=1e-3):
     """(HIP FusionTrainer on cuda:0, OracleTrainer on CPU) with identical initial weights and dropout masks."""
     torch.manual_seed(seed)
     bc = BertConfig(vocab_size=cfg["vocab"], hidden_size=cfg["D"], num_hidden_layers=cfg["layers"],
-                    num_attention_heads=cfg["heads"], intermediate_size=cfg["inter"], max_position_embeddings=64,
+                    num_attention_heads=cfg["heads"], intermediate_size=cfg["inter"],
+                    max_position_embeddings=max(64, cfg["seq"]),
                     hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)
     vc = ViTConfig(image_size=cfg["img"], patch_size=cfg["patch"], hidden_size=cfg["D"],
                    num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"], intermediate_size=cfg["inter"])
@@ -73,8 +77,10 @@ def _named_ref(ref):
     return out
 
 
-def compare_step(tr, ref, batch, loss_tol, grad_rtol):
-    """One step on each; returns (max loss err, worst grad error relative to that tensor's max |grad|)."""
+def compare_step(tr, ref, batch, loss_tol, grad_rtol, norm_rtol=None, report=None):
+    """One step on each; returns (max loss err, worst grad error relative to that tensor's max
+    |grad|). With `norm_rtol`, every gradient must also satisfy ||g - r||_2 / ||r||_2 <= norm_rtol;
+    `report` (a list) receives (name, max-relative, norm-relative) per tensor."""
     dev = torch.device("cuda", 0)
     tr.text_encoder.manual_seed(99)  # the oracle's make_drop(99, p) masks, every step
     tr.head.manual_seed(99)
@@ -91,16 +97,23 @@ def compare_step(tr, ref, batch, loss_tol, grad_rtol):
     # gradients that are zero in exact arithmetic (e.g. key biases: softmax is shift invariant)
     # are fp32 noise in both; judge every tensor against at least 1e-3 of the largest gradient
     floor = 1e-3 * max(r.grad.abs().max().item() for r in theirs.values() if r.grad is not None)
+    nfloor = 1e-3 * max(r.grad.norm().item() for r in theirs.values() if r.grad is not None)
+    fails = []
     for k, p in mine.items():
         g, r = p.grad, theirs[k].grad
         if r is None:
             assert g is None or g.abs().max().item() == 0.0, k
             continue
         assert g is not None, f"missing grad {k}"
-        scale = max(r.abs().max().item(), floor)
-        e = (g.double().cpu() - r.double()).abs().max().item() / scale
-        assert e <= grad_rtol, f"grad {k}: rel err {e:.2e} > {grad_rtol:.1e}"
+        d = g.double().cpu() - r.double()
+        e = d.abs().max().item() / max(r.abs().max().item(), floor)
+        en = d.norm().item() / max(r.double().norm().item(), nfloor)
+        if report is not None:
+            report.append((k, e, en))
+        if e > grad_rtol or (norm_rtol is not None and en > norm_rtol):
+            fails.append(f"grad {k}: max-rel {e:.2e} (bound {grad_rtol:.1e}), norm-rel {en:.2e} (bound {norm_rtol})")
         worst = max(worst, e)
+    assert not fails, "; ".join(fails[:8])
     return lerr, worst
 
 

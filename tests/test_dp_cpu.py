@@ -86,3 +86,53 @@ def test_grad_allreduce_gloo_world2(bucket_mb):
         want = sum(torch.randn(p.shape, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
         for r in range(world):
             torch.testing.assert_close(res[r][6 + i], want, rtol=1e-6, atol=1e-6)
+
+
+def _train_worker(rank, world, port, q):
+    """Replicas initialised from DIFFERENT seeds, different data per rank: after the rank-0
+    broadcast and two averaged steps every rank must hold bitwise-identical parameters."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.dp import GradAllReduce
+
+        torch.manual_seed(100 + rank)
+        m = torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.GELU(), torch.nn.Linear(16, 3))
+        dp = GradAllReduce(bucket_mb=0.0005, pack=_pack, unpack=_unpack)
+        dp.broadcast_params(list(m.parameters()))
+        init = [p.detach().clone().numpy() for p in m.parameters()]
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-2)
+        g = torch.Generator().manual_seed(7 + rank)
+        for _ in range(2):
+            opt.zero_grad(set_to_none=True)
+            x = torch.randn(8, 5, generator=g)
+            y = torch.randint(0, 3, (8,), generator=g)
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            dp.allreduce_grads(list(m.parameters()))
+            opt.step()
+        q.put((rank, init, [p.detach().clone().numpy() for p in m.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replicas_from_different_seeds_stay_identical():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, init, final = q.get(timeout=120)
+        res[r] = (init, final)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(100)  # rank 0's initialisation is the one every rank must hold
+    m0 = torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.GELU(), torch.nn.Linear(16, 3))
+    for a, b, p0 in zip(res[0][0], res[1][0], m0.parameters()):
+        assert (a == b).all() and (a == p0.detach().numpy()).all()
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a == b).all()
+    assert any((a != b).any() for a, b in zip(res[0][0], res[0][1]))  # and training moved them

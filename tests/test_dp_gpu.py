@@ -1,7 +1,9 @@
 """Data-parallel training step on the HIP path: 2 ranks (gloo, both on cuda:0 — the box has one
 GPU) each run FusionTrainer.step on half of a batch with the overlapped gradient all-reduce; the
-averaged gradients must equal the single-process gradients of the full batch (fp32, dropout off;
-the loss is a batch mean, so mean-of-halves == full-batch gradient up to fp32 rounding).
+ranks build their replicas from DIFFERENT seeds and FusionTrainer broadcasts rank 0's weights.
+The averaged gradients must equal the single-process gradients of the full batch (fp32, dropout
+off; the loss is a batch mean, so mean-of-halves == full-batch gradient up to fp32 rounding), and
+after a second step both replicas hold bitwise-identical parameters.
 Tolerance: 2e-4 relative to each tensor's max |grad| (the floor of tests/smoke_impl.compare_step).
 """
 import os
@@ -45,16 +47,22 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mmfd.dp import GradAllReduce
+        from mmfd.train import FusionTrainer
         from tests.smoke_impl import build_pair, tiny_batch
-        tr, _ = build_pair("fp32", dropout=0.0)
+        # each rank initialises from its OWN seed: FusionTrainer broadcasts rank 0's weights
+        t0, _ = build_pair("fp32", dropout=0.0, seed=5 + 11 * rank)
         dp = GradAllReduce(bucket_mb=0.05)  # many buckets -> several in flight during backward
-        for m in (tr.text_encoder, tr.image_encoder, tr.head):
-            m._grad_ready = dp.hook_for(m)
-        tr.dp = dp
+        tr = FusionTrainer(t0.text_encoder, t0.image_encoder, t0.head, lr=1e-3, precision="fp32", dp=dp)
         b = _half(tiny_batch(4, seed=21), rank, world)
         tr.step({k: v.cuda() for k, v in b.items()})
         torch.cuda.synchronize()
-        q.put((rank, _grads(tr)))
+        g1 = _grads(tr)
+        tr.step({k: v.cuda() for k, v in _half(tiny_batch(4, seed=22), rank, world).items()})
+        torch.cuda.synchronize()
+        params = {k: v.detach().cpu().numpy().copy() for m, pre in ((tr.text_encoder, "bert."), (tr.image_encoder, "vit."),
+                                                                      (tr.head, "head.")) for k, v in
+                  ((pre + n, p) for n, p in m.named_parameters())}
+        q.put((rank, g1, params))
     finally:
         dist.destroy_process_group()
 
@@ -67,10 +75,15 @@ def test_dp_two_ranks_match_full_batch():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
+    res, params = {}, {}
+    for _ in range(world):
+        r, g1, pr = q.get(timeout=300)
+        res[r], params[r] = g1, pr
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    for k in params[0]:  # replicas started from different seeds, trained 2 steps: identical
+        assert (params[0][k] == params[1][k]).all(), k
     tr, _ = build_pair("fp32", dropout=0.0)
     tr.step({k: v.cuda() for k, v in tiny_batch(4, seed=21).items()})
     torch.cuda.synchronize()

@@ -379,6 +379,55 @@ def test_seq_mean_xent():
         assert torch.allclose(dl[i].double().cpu(), lr[i].grad, atol=1e-6)
 
 
+def test_xent_absent_paths_use_reference_label_columns():
+    """train.py:163-167: path idx is trained on labels[:, idx] whatever other paths are None
+    (the kernel used the position in the shortened list)."""
+    from mmfd.train import path_losses
+    logits = [_rand(6, 3, seed=70 + i) for i in range(2)]
+    labels = torch.randint(0, 3, (6, 4), generator=torch.Generator().manual_seed(3))
+    outs = ((None, logits[0].to(DEV).requires_grad_(True)), (None, logits[1].to(DEV).requires_grad_(True)))
+    loss = path_losses(outs, labels.to(DEV))
+    loss[0].backward()
+    torch.cuda.synchronize()
+    lr = [l.double().requires_grad_(True) for l in logits]
+    l1 = torch.nn.functional.cross_entropy(lr[0], labels[:, 1])
+    l3 = torch.nn.functional.cross_entropy(lr[1], labels[:, 3])
+    (l1 + l3).backward()
+    got = loss.detach().cpu().double()
+    want = torch.tensor([(l1 + l3).item(), 0.0, l1.item(), 0.0, l3.item()], dtype=torch.float64)
+    assert (got - want).abs().max().item() < 1e-5, (got, want)
+    assert torch.allclose(outs[0][1].grad.double().cpu(), lr[0].grad, atol=1e-6)
+    assert torch.allclose(outs[1][1].grad.double().cpu(), lr[1].grad, atol=1e-6)
+
+
+def test_adamw_loads_torch_optimizer_state():
+    """A torch.optim.AdamW state_dict (CPU 'step' tensors) loads into mmfd AdamW and the
+    next step matches torch continuing from the same state."""
+    from mmfd.optim import AdamW
+    ps = [_rand(300, seed=80), _rand(7, 11, seed=81)]
+    gs = [_rand(300, seed=82), _rand(7, 11, seed=83)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    for r, g in zip(ref, gs):
+        r.grad = g.clone()
+    opt.step()
+    import copy
+    sd = copy.deepcopy(opt.state_dict())  # as read back from a checkpoint file (no shared tensors)
+    dev = [r.detach().clone().to(DEV).requires_grad_(True) for r in ref]
+    mine = AdamW(dev, lr=1e-3, weight_decay=0.01)
+    mine.load_state_dict(sd)
+    assert mine.state[dev[0]]["step"].device.type == "cpu"  # torch leaves it where it was loaded
+    for r, d, g in zip(ref, dev, gs):
+        r.grad = 2 * g
+        d.grad = (2 * g).to(DEV)
+    opt.step()
+    mine.step()
+    torch.cuda.synchronize()
+    for r, d in zip(ref, dev):
+        assert (r.detach() - d.detach().cpu()).abs().max().item() < 1e-6
+    assert mine.state[dev[0]]["step"].device == dev[0].device and float(mine.state[dev[0]]["step"]) == 2.0
+
+
 def test_adamw_matches_torch():
     ps = [_rand(1000, seed=60), _rand(37, 5, seed=61)]
     gs = [_rand(1000, seed=62), _rand(37, 5, seed=63)]
