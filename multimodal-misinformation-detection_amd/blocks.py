@@ -48,6 +48,38 @@ def shadow_store(module):
     return st
 
 
+def invalidate_caches(module):
+    """Drop every weight-derived tensor of `module` (compute-dtype shadows, packed biases, position-
+    bias tables): the next forward rebuilds them from the master parameters. Needed after writes
+    that bypass torch's version counter (`p.data.copy_(...)`, `p.data[...] = ...`);
+    load_state_dict / .to() / .cuda() call it themselves (CachedWeights)."""
+    st = module.__dict__.get("_mmfd_shadows")
+    if st:
+        sid = id(st)
+        for ptr in [k for k, v in SHADOW_OF.items() if v[1][0] == sid]:
+            del SHADOW_OF[ptr]
+        st.clear()
+
+
+class CachedWeights:
+    """Mixin for nn.Modules that keep weight-derived caches (shadow_store): invalidated by
+    load_state_dict and by _apply (.to / .cuda / .float ...), and on demand by invalidate_caches()."""
+
+    def invalidate_caches(self):
+        invalidate_caches(self)
+        return self
+
+    def load_state_dict(self, *a, **kw):
+        r = super().load_state_dict(*a, **kw)
+        invalidate_caches(self)
+        return r
+
+    def _apply(self, *a, **kw):
+        r = super()._apply(*a, **kw)
+        invalidate_caches(self)
+        return r
+
+
 class StepCtx:
     def __init__(self, params: dict, dtype: torch.dtype, dropout_p: float = 0.0, seed: K.Seed | None = None,
                  training: bool = False, shadows: dict | None = None):
@@ -166,9 +198,10 @@ class StepCtx:
     def derived(self, key, pnames, make):
         """a tensor computed from the parameters `pnames` only (packed biases, Swinv2 position-bias
         tables), kept in the module's persistent store and rebuilt when any of them changed
-        (data pointer or version counter). Opt-in per context (`cache_derived`): only for frozen,
-        inference-only encoders — mmfd's AdamW writes parameters through raw pointers without
-        bumping torch's version counter, so training contexts always rebuild."""
+        (data pointer or version counter), and dropped by invalidate_caches() / load_state_dict.
+        Opt-in per context (`cache_derived`): only for frozen, inference-only encoders — mmfd's
+        AdamW writes parameters through raw pointers without bumping torch's version counter, so
+        training contexts always rebuild."""
         if self.shadows is None or not self.cache_derived:
             return make()
         sig = tuple((self.P[n].data_ptr(), self.P[n]._version) for n in pnames)

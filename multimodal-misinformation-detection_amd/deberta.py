@@ -80,7 +80,7 @@ def _bias_indices(L, S, max_position, device):
     return t
 
 
-class DebertaV2Model(nn.Module):
+class DebertaV2Model(Bk.CachedWeights, nn.Module):
     def __init__(self, config: DebertaV2Config | None = None, **kw):
         super().__init__()
         c = config or DebertaV2Config(**kw)

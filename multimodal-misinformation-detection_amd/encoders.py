@@ -57,7 +57,7 @@ class EncoderOutput:
 # -------------------------------------------------------------------------------------------------
 # BERT
 # -------------------------------------------------------------------------------------------------
-class BertModel(nn.Module):
+class BertModel(Bk.CachedWeights, nn.Module):
     """HF BertModel (add_pooling_layer=False) parameter layout; forward returns .last_hidden_state."""
 
     def __init__(self, config: BertConfig | None = None, **kw):
@@ -245,7 +245,7 @@ class _BertFn(torch.autograd.Function):
 # -------------------------------------------------------------------------------------------------
 # ViT
 # -------------------------------------------------------------------------------------------------
-class ViTModel(nn.Module):
+class ViTModel(Bk.CachedWeights, nn.Module):
     """HF ViTModel (add_pooling_layer=False) with hub parameter names; forward(pixel_values)."""
 
     def __init__(self, config: ViTConfig | None = None, **kw):
@@ -433,7 +433,7 @@ def mpnet_relative_buckets(L, num_buckets=32, max_distance=128):
     return ret.to(torch.int32)
 
 
-class MPNetModel(nn.Module):
+class MPNetModel(Bk.CachedWeights, nn.Module):
     """HF MPNetModel (add_pooling_layer=False) parameter layout; forward(input_ids, attention_mask)
     returns .last_hidden_state. Inference only (the corpus extractor never trains it)."""
 

@@ -13,10 +13,21 @@ a13  MPNet sentence embeddings — the reference's `TextCorpus.encode_corpus` (t
 
 Pretrained checkpoints cannot be downloaded here: models are randomly initialised unless a
 state_dict is given (torchvision / HF names load unchanged).
+
+Corpus build (config 5): images are decoded on the host (PIL), preprocessed on the GPU in batches
+(mmfd.preprocess, bit-exact with the reference's torchvision transform) and embedded in batches;
+with torch.distributed initialised (or an explicit shard=(rank, world)) every rank embeds one
+contiguous shard of the sorted corpus and writes its own shard file, and rank 0 merges them — no
+collective on the data path. The reference's pickle corpus (path -> fp32 [2048] tensor,
+im2im_retrieval.py:51-58, 78) is read with a restricted unpickler that only rebuilds tensors
+(`load_corpus_pickle`) and written in the same format.
 """
 from __future__ import annotations
 
+import collections
+import io
 import os
+import pickle
 
 import numpy as np
 import torch
@@ -27,6 +38,75 @@ from .encoders import MPNetConfig, MPNetModel
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+# -------------------------------------------------------------------------------------------------
+# corpus files: the reference's pickle (path -> tensor) through an unpickler that executes nothing
+# but tensor reconstruction, and shard bookkeeping
+# -------------------------------------------------------------------------------------------------
+def _storage_from_bytes(data):
+    import torch as _t
+    return _t.load(io.BytesIO(data), weights_only=True)
+
+
+_CORPUS_ALLOWED = {
+    ("torch._utils", "_rebuild_tensor_v2"): torch._utils._rebuild_tensor_v2,
+    ("torch.storage", "_load_from_bytes"): _storage_from_bytes,
+    ("collections", "OrderedDict"): collections.OrderedDict,
+}
+
+
+class _CorpusUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        fn = _CORPUS_ALLOWED.get((module, name))
+        if fn is None:
+            raise pickle.UnpicklingError(f"corpus pickle references {module}.{name}: only tensors are allowed")
+        return fn
+
+
+def load_corpus_pickle(path):
+    """The reference's feature corpus (pickle.dump of {path: tensor}, im2im_retrieval.py:51-58, 78)
+    -> dict; tensors are rebuilt with torch.load(weights_only=True), any other global refuses."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if not data:
+        return {}
+    d = _CorpusUnpickler(io.BytesIO(data)).load()
+    if not isinstance(d, dict):
+        raise pickle.UnpicklingError("corpus pickle does not hold a dict")
+    return d
+
+
+def save_corpus_pickle(path, feature_dict):
+    """same format as the reference's save_features (im2im_retrieval.py:60-62)"""
+    with open(path, "wb") as f:
+        pickle.dump({k: torch.as_tensor(v).detach().cpu() for k, v in feature_dict.items()}, f)
+
+
+def dist_shard():
+    """(rank, world) of the initialised default process group, else (0, 1)"""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_range(n, rank, world):
+    """contiguous [lo, hi) of n items for `rank` (the first n % world ranks take one more)"""
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (rank < r)
+
+
+def shard_path(path, rank, world):
+    root, ext = os.path.splitext(path)
+    return f"{root}.shard{rank}-of-{world}{ext}"
+
+
+def _barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
 
 
 # -------------------------------------------------------------------------------------------------
@@ -90,6 +170,16 @@ class ResNet(nn.Module):
         self.compute_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
         self._prep = None
         return self
+
+    def invalidate_caches(self):
+        """drop the folded GEMM weights (after writes that bypass torch's version counter)"""
+        self._prep = None
+        return self
+
+    def load_state_dict(self, *a, **kw):
+        r = super().load_state_dict(*a, **kw)
+        self._prep = None
+        return r
 
     # ---- folded GEMM weights (recomputed when any parameter/buffer changes) --------------------
     def _prepared(self):
@@ -167,16 +257,12 @@ def resnet50(**kw):
 # -------------------------------------------------------------------------------------------------
 # image preprocessing (im2im_retrieval.py:19-27) and the extractor API
 # -------------------------------------------------------------------------------------------------
-def preprocess(image, size=224):
-    """PIL image (or path / stream) -> fp32 [3, size, size]: Resize((size, size)) bilinear ->
-    ToTensor -> Normalize(ImageNet mean/std). Host side (as torchvision does on PIL images)."""
+def _decode(image):
+    """host decode (PIL) -> RGB PIL image"""
     from PIL import Image
     if not isinstance(image, Image.Image):
         image = Image.open(image)
-    image = image.convert("RGB").resize((size, size), Image.BILINEAR)
-    a = np.asarray(image, dtype=np.float32) / 255.0
-    a = (a - np.asarray(IMAGENET_MEAN, np.float32)) / np.asarray(IMAGENET_STD, np.float32)
-    return torch.from_numpy(a.transpose(2, 0, 1).copy())
+    return image.convert("RGB")
 
 
 class ImageSimilarity:
@@ -189,13 +275,23 @@ class ImageSimilarity:
             self.model.load_state_dict(state_dict, strict=False)
         self.model = self.model.to(device).eval().set_precision(precision)
         self.device = device
+        self._pre = None
+
+    def preprocess_batch(self, images):
+        """decoded images (PIL / uint8 HWC) -> normalised fp32 [N, 3, 224, 224] on the device: the
+        transform of im2im_retrieval.py:19-27 on the GPU (mmfd.preprocess "retrieval", bit-exact)"""
+        if self._pre is None:
+            from .preprocess import ImagePreprocessor
+            self._pre = ImagePreprocessor("retrieval", device=self.device)
+        return self._pre(images)
 
     def extract_batch(self, pixels):
         """normalised fp32 [N, 3, 224, 224] (host or device) -> fp32 [N, 2048] on the device"""
         return self.model(pixels).flatten(1)
 
     def extract_features(self, image_stream):
-        x = preprocess(image_stream).unsqueeze(0)
+        """im2im_retrieval.py:29-36: one image (path / stream) -> fp32 [2048] (host)"""
+        x = self.preprocess_batch([_decode(image_stream)])
         return self.extract_batch(x).flatten().cpu()
 
     @staticmethod
@@ -206,46 +302,94 @@ class ImageSimilarity:
 
 
 class ImageCorpus:
-    """im2im_retrieval.py:45-78 with batched extraction. Features persist as an .npz archive
-    (`paths`, `features` [N, 2048] fp32) instead of a pickle."""
+    """im2im_retrieval.py:45-78 with batched GPU extraction. The corpus file is the reference's
+    pickle (path -> fp32 [2048] tensor) unless its name ends in .npz (`paths`, `features`)."""
 
     def __init__(self, feature_corpus_path, extractor: ImageSimilarity | None = None, batch_size=256):
         self.feature_corpus_path = feature_corpus_path
         self.feature_extractor = extractor or ImageSimilarity()
         self.batch_size = batch_size
         self.feature_dict = self.load_features()
+        self._revision = 0  # bumped on every feature_dict write: the device index is rebuilt
+
+    @staticmethod
+    def _read(path):
+        if not os.path.exists(path):
+            return {}
+        if path.endswith(".npz"):
+            z = np.load(path, allow_pickle=False)
+            return {p: torch.from_numpy(f) for p, f in zip(z["paths"].tolist(), z["features"])}
+        return load_corpus_pickle(path)
+
+    @staticmethod
+    def _write(path, feature_dict):
+        if path.endswith(".npz"):
+            paths = list(feature_dict)
+            feats = (np.stack([torch.as_tensor(feature_dict[p]).numpy() for p in paths]) if paths
+                     else np.zeros((0, 2048), np.float32))
+            with open(path, "wb") as f:
+                np.savez(f, paths=np.array(paths), features=feats)
+        else:
+            save_corpus_pickle(path, feature_dict)
 
     def load_features(self):
-        if not os.path.exists(self.feature_corpus_path):
-            return {}
-        z = np.load(self.feature_corpus_path, allow_pickle=False)
-        return {p: torch.from_numpy(f) for p, f in zip(z["paths"].tolist(), z["features"])}
+        return self._read(self.feature_corpus_path)
 
     def save_features(self):
-        paths = list(self.feature_dict)
-        feats = np.stack([self.feature_dict[p].numpy() for p in paths]) if paths else np.zeros((0, 2048), np.float32)
-        with open(self.feature_corpus_path, "wb") as f:
-            np.savez(f, paths=np.array(paths), features=feats)
+        self._write(self.feature_corpus_path, self.feature_dict)
 
     def add_image(self, image_path):
         self.feature_dict[image_path] = self.feature_extractor.extract_features(image_path)
+        self._revision += 1
         self.save_features()
 
-    def create_feature_corpus(self, image_dir):
-        paths = [os.path.join(image_dir, n) for n in sorted(os.listdir(image_dir))]
-        paths = [p for p in paths if os.path.isfile(p) and p.lower().endswith((".png", ".jpg", ".jpeg"))]
+    def _extract_paths(self, paths):
+        out = {}
         for i in range(0, len(paths), self.batch_size):
             chunk = paths[i:i + self.batch_size]
-            px = torch.stack([preprocess(p) for p in chunk])
-            feats = self.feature_extractor.extract_batch(px).cpu()
+            px = self.feature_extractor.preprocess_batch([_decode(p) for p in chunk])
+            feats = self.feature_extractor.extract_batch(px).float().cpu()
             for p, f in zip(chunk, feats):
-                self.feature_dict[p] = f
+                out[p] = f.clone()
+        return out
+
+    def create_feature_corpus(self, image_dir, shard=None):
+        """im2im_retrieval.py:69-78 over the .png/.jpg/.jpeg files of image_dir, in batches. With a
+        process group (or shard=(rank, world)) each rank embeds its contiguous shard of the sorted
+        file list into `<corpus>.shard<r>-of-<w>` and rank 0 merges the shards into the corpus."""
+        paths = [os.path.join(image_dir, n) for n in sorted(os.listdir(image_dir))]
+        paths = [p for p in paths if os.path.isfile(p) and p.lower().endswith((".png", ".jpg", ".jpeg"))]
+        rank, world = shard if shard is not None else dist_shard()
+        if world == 1:
+            self.feature_dict.update(self._extract_paths(paths))
+            self._revision += 1
+            self.save_features()
+            return self.feature_corpus_path
+        lo, hi = shard_range(len(paths), rank, world)
+        self._write(shard_path(self.feature_corpus_path, rank, world), self._extract_paths(paths[lo:hi]))
+        if shard is None:
+            _barrier()
+            if rank == 0:
+                self.merge_shards(world)
+            _barrier()
+            self.feature_dict = self.load_features()
+            self._revision += 1
+        return shard_path(self.feature_corpus_path, rank, world)
+
+    def merge_shards(self, world, remove=True):
+        """rank 0: concatenate the per-rank shard files (in rank order) into the corpus file"""
+        for r in range(world):
+            sp = shard_path(self.feature_corpus_path, r, world)
+            self.feature_dict.update(self._read(sp))
+            if remove:
+                os.remove(sp)
+        self._revision += 1
         self.save_features()
 
     def index(self):
         """The corpus features as a device-resident CorpusIndex (rebuilt when the corpus changed)."""
         from .retrieval import CorpusIndex
-        key = (len(self.feature_dict), next(reversed(self.feature_dict)) if self.feature_dict else None)
+        key = (id(self.feature_dict), self._revision, len(self.feature_dict))
         if getattr(self, "_index_key", None) != key:
             paths = list(self.feature_dict)
             feats = torch.stack([self.feature_dict[p].float().flatten() for p in paths])
@@ -304,18 +448,67 @@ class TextCorpus:
         self.split, self.data_dir = split, data_dir
         self.out_dir = out_dir or data_dir
 
-    def encode_corpus(self):
+    def encode_corpus(self, shard=None):
+        """text2text_retrieval.py:129-157. With a process group (or shard=(rank, world)) each rank
+        encodes its contiguous shard of the CSV rows into a shard file and rank 0 concatenates the
+        shards (rank order = row order) into `{split}_embeddings.{h5|npz}`."""
         import pandas as pd
         df = pd.read_csv(os.path.join(self.data_dir, f"{self.split}_enriched.csv"))
-        emb = self.bi_encoder.encode(df["evidence_enriched"].tolist()).numpy().astype(np.float16)
+        texts = df["evidence_enriched"].tolist()
         ids = [f"{self.split}_{i}" for i in df["id"].tolist()]
+        rank, world = shard if shard is not None else dist_shard()
+        lo, hi = shard_range(len(texts), rank, world)
+        emb = self.bi_encoder.encode(texts[lo:hi]).numpy().astype(np.float16) if hi > lo else \
+            np.zeros((0, 768), np.float16)
+        path = self.output_path()
+        if world == 1:
+            return self._write(path, emb, ids)
+        self._write(shard_path(path, rank, world), emb, ids[lo:hi])
+        if shard is None:
+            _barrier()
+            if rank == 0:
+                self.merge_shards(world)
+            _barrier()
+        return path if shard is None else shard_path(path, rank, world)
+
+    def output_path(self):
         try:
+            import h5py  # noqa: F401
+            ext = "h5"
+        except ImportError:
+            ext = "npz"
+        return os.path.join(self.out_dir, f"{self.split}_embeddings.{ext}")
+
+    @staticmethod
+    def _write(path, emb, ids):
+        if path.endswith(".h5"):
             import h5py
-            path = os.path.join(self.out_dir, f"{self.split}_embeddings.h5")
             with h5py.File(path, "w") as h5:
                 h5.create_dataset("embeddings", data=emb, dtype="float16")
                 h5.create_dataset("ids", data=ids, dtype=h5py.string_dtype())
-        except ImportError:
-            path = os.path.join(self.out_dir, f"{self.split}_embeddings.npz")
-            np.savez(path, embeddings=emb, ids=np.array(ids))
+        else:
+            with open(path, "wb") as f:
+                np.savez(f, embeddings=emb, ids=np.array(ids, dtype=str))
         return path
+
+    @staticmethod
+    def read(path):
+        """(fp16 embeddings [N, 768], ids) of an embeddings file (text2text_retrieval.py:39-47)"""
+        if path.endswith(".h5"):
+            import h5py
+            with h5py.File(path, "r") as h5:
+                return h5["embeddings"][()], [x.decode() if isinstance(x, bytes) else x for x in h5["ids"][()]]
+        z = np.load(path, allow_pickle=False)
+        return z["embeddings"], z["ids"].tolist()
+
+    def merge_shards(self, world, remove=True):
+        path = self.output_path()
+        embs, ids = [], []
+        for r in range(world):
+            sp = shard_path(path, r, world)
+            e, i = self.read(sp)
+            embs.append(e)
+            ids += list(i)
+            if remove:
+                os.remove(sp)
+        return self._write(path, np.concatenate(embs) if embs else np.zeros((0, 768), np.float16), ids)

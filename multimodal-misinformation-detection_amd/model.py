@@ -153,7 +153,7 @@ class _HeadFn(torch.autograd.Function):
         return (None, *dxs, *pgrads)
 
 
-class MisinformationDetectionModel(nn.Module):
+class MisinformationDetectionModel(Bk.CachedWeights, nn.Module):
     """model.py:350-468. forward(X_t, X_i, E_t, E_i) -> ((y_tt, y_ti), (y_it, y_ii)) or (pred, None)."""
 
     def __init__(self, text_input_dim=768, image_input_dim=1024, embed_dim=256, num_heads=8, dropout=0.1,

@@ -57,7 +57,15 @@ class MisinformationPredictor:
         (ytt, yti), (yit, yii) = self.model(T[:1], I[:1], T[1:], I[1:])
         return ytt, yti, yit, yii
 
+    def _signature(self):
+        """(data_ptr, version) of every parameter and buffer the captured forward reads: a graph
+        is baked with the addresses of the weight shadows / packed biases built from them, so any
+        change (load_state_dict, optimizer outside mmfd's AdamW, .to()) forces a re-capture."""
+        return tuple((t.data_ptr(), t._version) for m in (self.text_encoder, self.image_encoder, self.model)
+                     for t in (*m.parameters(), *m.buffers()))
+
     def _capture(self):
+        self._sig = self._signature()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -91,7 +99,8 @@ class MisinformationPredictor:
         """((y_tt, y_ti), (y_it, y_ii)) logits [1, num_classes] for one pair (model.py:426-468)."""
         self._load(claim_ids, claim_mask, claim_pixels, evidence_ids, evidence_mask, evidence_pixels)
         if self.use_graph:
-            if self._graph is None:
+            if self._graph is None or self._sig != self._signature():
+                self._graph = None
                 self._capture()
             self._graph.replay()
             out = self._out

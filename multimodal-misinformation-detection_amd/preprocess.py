@@ -5,7 +5,10 @@ fp32 NCHW pixel tensor, bit-identical to the reference's torchvision transforms 
     the longer one int(256 * long / short)), CenterCrop(256), ToTensor, Normalize(mean 0.5,
     std ImageNet);
   * mode "retrieval": the ImageSimilarity transform of src/evidence/im2im_retrieval.py:19-27 —
-    Resize((224, 224)), ToTensor, Normalize(ImageNet mean / std).
+    Resize((224, 224)), ToTensor, Normalize(ImageNet mean / std);
+  * mode "evaluate": MisinformationPredictor's image_transform of evaluate.py:71-79 —
+    Resize((256, 256)), ToTensor, Normalize(ImageNet mean / std).
+`size=` overrides the (square) resize of the fixed-size modes, e.g. 224 for a ViT-B/16 predictor.
 
 torchvision resizes PIL images with PIL's Image.resize(BILINEAR). Its taps are computed here on the
 host exactly as PIL computes them (double precision, 22-bit fixed point; cached per (in, out)
@@ -28,6 +31,7 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 MODES = {
     "train": dict(resize=256, crop=256, mean=(0.5, 0.5, 0.5), std=IMAGENET_STD),   # dataset.py:14-19
     "retrieval": dict(resize=(224, 224), crop=None, mean=IMAGENET_MEAN, std=IMAGENET_STD),  # im2im:19-27
+    "evaluate": dict(resize=(256, 256), crop=None, mean=IMAGENET_MEAN, std=IMAGENET_STD),   # evaluate.py:71-79
 }
 _PB = 22  # PIL PRECISION_BITS (8-bit images)
 
@@ -98,10 +102,14 @@ class ImagePreprocessor:
     """Batch preprocessing on the GPU: __call__(list of PIL images / uint8 HWC arrays) -> fp32
     [N, 3, S, S] on `device`."""
 
-    def __init__(self, mode="train", device="cuda"):
+    def __init__(self, mode="train", device="cuda", size=None):
         if mode not in MODES:
             raise ValueError(f"mode must be one of {list(MODES)}")
-        self.mode, self.cfg, self.device = mode, MODES[mode], torch.device(device)
+        self.mode, self.cfg, self.device = mode, dict(MODES[mode]), torch.device(device)
+        if size is not None:
+            if self.cfg["crop"]:
+                raise ValueError("size= applies to the fixed-size modes (retrieval / evaluate)")
+            self.cfg["resize"] = (int(size), int(size))
         c = self.cfg
         self.out_hw = (c["crop"], c["crop"]) if c["crop"] else tuple(c["resize"])
         self._mean = (ctypes.c_float * 3)(*c["mean"])

@@ -145,7 +145,7 @@ def _linear(i, o, bias=True):
     return nn.Linear(i, o, bias=bias)
 
 
-class Swinv2Model(nn.Module):
+class Swinv2Model(Bk.CachedWeights, nn.Module):
     def __init__(self, config: Swinv2Config | None = None, **kw):
         super().__init__()
         c = config or Swinv2Config(**kw)

@@ -3,7 +3,8 @@ bench.py's cpu_baseline, never by the product path).
 
 Restates torchvision's transforms as the reference composes them — Resize(256) + CenterCrop(256)
 + ToTensor + Normalize(mean 0.5, ImageNet std) at src/model/dataset.py:14-19, and
-Resize((224, 224)) + ToTensor + Normalize(ImageNet) at src/evidence/im2im_retrieval.py:19-27 —
+Resize((224, 224)) + ToTensor + Normalize(ImageNet) at src/evidence/im2im_retrieval.py:19-27, and
+Resize((256, 256)) + ToTensor + Normalize(ImageNet) at evaluate.py:71-79 —
 on top of PIL itself: torchvision (pinned 0.20.1, absent here) resizes PIL images with
 Image.resize(BILINEAR), crops with Image.crop, converts with np.asarray / 255 in fp32 and
 normalises with fp32 sub / div, so PIL (importable here and on the GPU box) is the reference's

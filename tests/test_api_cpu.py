@@ -142,3 +142,27 @@ def test_stepctx_derived_cache_tracks_weight_versions():
     ctx = Bk.StepCtx({"w": w}, torch.float32, shadows=store)      # cache_derived off (training)
     ctx.derived("k", ["w"], make)
     assert len(calls) == 3
+
+
+def test_cached_weights_invalidate_on_load_state_dict_and_data_writes():
+    """weight-derived caches (shadow_store) are dropped by load_state_dict, .to() and an
+    explicit invalidate_caches() (writes through .data do not bump torch's version counter)."""
+    from mmfd import blocks as Bk
+    from mmfd.model import MisinformationDetectionModel
+
+    m = MisinformationDetectionModel(text_input_dim=16, image_input_dim=16, embed_dim=8, num_heads=2, hidden_dim=4)
+    st = Bk.shadow_store(m)
+    st["k"] = (torch.zeros(1), [])
+    st[("derived", "x")] = ((), torch.zeros(1))
+    m.load_state_dict(m.state_dict())
+    assert not Bk.shadow_store(m)
+    st = Bk.shadow_store(m)
+    st["k"] = (torch.zeros(1), [])
+    with torch.no_grad():
+        next(m.parameters()).data.copy_(torch.ones_like(next(m.parameters())))
+    assert Bk.shadow_store(m)  # a .data write is invisible to version counters ...
+    m.invalidate_caches()
+    assert not Bk.shadow_store(m)  # ... hence the explicit call
+    Bk.shadow_store(m)["k"] = (torch.zeros(1), [])
+    m.float()
+    assert not Bk.shadow_store(m)

@@ -1,0 +1,150 @@
+"""Evidence-corpus files and rank sharding on the CPU (no GPU calls).
+
+* the reference's pickle corpus (pickle.dump of {path: tensor}, im2im_retrieval.py:51-62, 78)
+  round-trips through mmfd's restricted unpickler, which refuses any other global;
+* create_feature_corpus sharded over a gloo world of 2 (contiguous shards of the sorted file list,
+  one shard file per rank, rank-0 merge) gives the same corpus as one process. The extractor is a
+  CPU stand-in here (the oracle's preprocessing + a fixed reduction): the code under test is the
+  sharding / file protocol, the HIP extractor itself is covered by tests/test_evidence_gpu.py.
+"""
+import os
+import pickle
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _StubExtractor:
+    device = "cpu"
+
+    def preprocess_batch(self, images):
+        from oracle.preprocess import preprocess
+        from mmfd.preprocess import MODES
+        c = MODES["retrieval"]
+        return torch.stack([torch.from_numpy(preprocess(im, c["resize"], None, c["mean"], c["std"])) for im in images])
+
+    def extract_batch(self, px):
+        return torch.cat([px.mean(dim=(2, 3)), px.amax(dim=(2, 3))], dim=1)
+
+    def extract_features(self, path):
+        from PIL import Image
+        return self.extract_batch(self.preprocess_batch([Image.open(path).convert("RGB")]))[0]
+
+
+def _images(d, n=7):
+    from PIL import Image
+    rng = np.random.default_rng(1)
+    for i in range(n):
+        Image.fromarray(rng.integers(0, 255, (30 + i, 41, 3), dtype=np.uint8)).save(os.path.join(d, f"im{i:02d}.jpg"))
+
+
+def test_reference_pickle_corpus_roundtrip_and_refusal(tmp_path):
+    from mmfd.evidence import ImageCorpus, load_corpus_pickle
+    feats = {f"/data/{i}.jpg": torch.randn(2048) for i in range(4)}
+    p = tmp_path / "corpus.pkl"
+    with open(p, "wb") as f:
+        pickle.dump(feats, f)  # exactly what the reference's save_features writes
+    got = load_corpus_pickle(str(p))
+    assert list(got) == list(feats) and all(torch.equal(got[k], feats[k]) for k in feats)
+    c = ImageCorpus(str(p), extractor=_StubExtractor())
+    assert set(c.feature_dict) == set(feats)
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned",))
+
+    bad = tmp_path / "bad.pkl"
+    with open(bad, "wb") as f:
+        pickle.dump({"x": Evil()}, f)
+    with pytest.raises(pickle.UnpicklingError):
+        load_corpus_pickle(str(bad))
+    (tmp_path / "empty.pkl").write_bytes(b"")
+    assert load_corpus_pickle(str(tmp_path / "empty.pkl")) == {}
+
+
+def test_shard_range_covers_everything_once():
+    from mmfd.evidence import shard_range
+    for n in (0, 1, 7, 64, 100003):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard_worker(rank, world, port, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.evidence import ImageCorpus
+        c = ImageCorpus(os.path.join(d, "sharded.pkl"), extractor=_StubExtractor(), batch_size=2)
+        c.create_feature_corpus(os.path.join(d, "imgs"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_corpus_build_equals_single_process(tmp_path):
+    from mmfd.evidence import ImageCorpus, load_corpus_pickle
+    os.makedirs(tmp_path / "imgs")
+    _images(str(tmp_path / "imgs"))
+    single = ImageCorpus(str(tmp_path / "single.pkl"), extractor=_StubExtractor(), batch_size=3)
+    single.create_feature_corpus(str(tmp_path / "imgs"))
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    merged = load_corpus_pickle(str(tmp_path / "sharded.pkl"))
+    assert list(merged) == list(single.feature_dict)  # sorted order, every file once
+    for k in merged:
+        assert torch.allclose(merged[k], single.feature_dict[k], atol=1e-6)
+    assert not [f for f in os.listdir(tmp_path) if ".shard" in f]  # shard files merged and removed
+
+
+class _StubTextEncoder:
+    def encode(self, texts):
+        return torch.tensor([[float(len(t)), float(sum(map(ord, t)) % 997)] + [0.0] * 766 for t in texts])
+
+
+def _text_worker(rank, world, port, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.evidence import TextCorpus
+        TextCorpus(d, "train", encoder=_StubTextEncoder(), out_dir=os.path.join(d, "sharded")).encode_corpus()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_text_corpus_equals_single_process(tmp_path):
+    import pandas as pd
+    from mmfd.evidence import TextCorpus
+    pd.DataFrame({"id": list(range(11)), "evidence_enriched": [f"evidence text {i} " * (i + 1) for i in range(11)]}
+                 ).to_csv(tmp_path / "train_enriched.csv", index=False)
+    os.makedirs(tmp_path / "single")
+    os.makedirs(tmp_path / "sharded")
+    one = TextCorpus(str(tmp_path), "train", encoder=_StubTextEncoder(), out_dir=str(tmp_path / "single")).encode_corpus()
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_text_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    e1, i1 = TextCorpus.read(one)
+    e2, i2 = TextCorpus.read(str(tmp_path / "sharded" / os.path.basename(one)))
+    assert i1 == i2 == [f"train_{i}" for i in range(11)]
+    assert e1.dtype == np.float16 and np.array_equal(e1, e2)

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 import mmfd
 from mmfd import kernels as K
 from mmfd.encoders import MPNetConfig, MPNetModel
-from mmfd.evidence import ImageCorpus, ImageSimilarity, ResNet, SentenceEncoder, preprocess, resnet50
+from mmfd.evidence import ImageCorpus, ImageSimilarity, ResNet, SentenceEncoder, resnet50
 from oracle import encoders as OE
 from oracle.resnet import resnet_forward
 
@@ -123,15 +123,20 @@ def test_image_similarity_and_corpus(tmp_path):
     buf.seek(0)
     assert torch.allclose(ext.extract_features(buf), f)
     assert abs(ImageSimilarity.similarity(f, f) - 1.0) < 1e-9
-    corpus = ImageCorpus(str(tmp_path / "feats.npz"), extractor=ext, batch_size=2)
-    corpus.create_feature_corpus(str(tmp_path))
-    assert len(corpus.feature_dict) == 5
-    again = ImageCorpus(str(tmp_path / "feats.npz"), extractor=ext)
-    assert set(again.feature_dict) == set(corpus.feature_dict)
-    p0 = str(tmp_path / "img0.png")
-    assert torch.allclose(again.feature_dict[p0], f, atol=1e-5)
+    for name in ("feats.npz", "feats.pkl"):  # .npz archive / the reference's pickle
+        corpus = ImageCorpus(str(tmp_path / name), extractor=ext, batch_size=2)
+        corpus.create_feature_corpus(str(tmp_path))
+        assert len(corpus.feature_dict) == 5
+        again = ImageCorpus(str(tmp_path / name), extractor=ext)
+        assert set(again.feature_dict) == set(corpus.feature_dict)
+        p0 = str(tmp_path / "img0.png")
+        assert torch.allclose(again.feature_dict[p0], f, atol=1e-5)
     # batched and single extraction agree
-    batch = torch.stack([preprocess(str(tmp_path / f"img{i}.png")) for i in range(5)])
+    from oracle.preprocess import preprocess
+    from mmfd.preprocess import MODES
+    c = MODES["retrieval"]
+    batch = torch.stack([torch.from_numpy(preprocess(Image.open(tmp_path / f"img{i}.png"), c["resize"], None, c["mean"],
+                                                     c["std"])) for i in range(5)])
     fb = ext.extract_batch(batch).cpu()
     assert (fb[0] - f).abs().max().item() < 1e-4
 

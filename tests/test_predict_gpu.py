@@ -83,3 +83,23 @@ def test_predictor_rejects_bad_pixels():
     c, e = _pair((8, 8), seed=3)
     with pytest.raises(ValueError):
         pr.predict_logits(c[0], c[1], torch.zeros(3, 32, 32), *e)
+
+
+def test_predictor_graph_recaptures_after_checkpoint_swap():
+    """a captured graph is baked with the addresses of the bf16 weight shadows; after a
+    load_state_dict of the head the graph is re-captured and equals the eager forward again."""
+    from mmfd.predict import MisinformationPredictor
+    from mmfd.train import build_flagship
+
+    tr = build_flagship("cuda", "bf16", seed=6)
+    c, e = _pair((40, 90), seed=13)
+    graph = MisinformationPredictor.from_trainer(tr, use_graph=True)
+    before = [y for pair in graph.predict_logits(*c, *e) for y in pair]
+    sd = {k: v * 1.5 if k.endswith("weight") else v for k, v in tr.head.state_dict().items()}
+    tr.head.load_state_dict(sd)
+    after = [y for pair in graph.predict_logits(*c, *e) for y in pair]
+    eager = MisinformationPredictor.from_trainer(tr, use_graph=False)
+    want = [y for pair in eager.predict_logits(*c, *e) for y in pair]
+    assert any(not torch.equal(a, b) for a, b in zip(before, after))
+    for a, b in zip(after, want):
+        assert torch.equal(a, b)

@@ -17,7 +17,7 @@ SIZES = [(375, 500), (500, 375), (256, 256), (256, 300), (300, 256), (100, 90), 
          (257, 1000)]
 
 
-@pytest.mark.parametrize("mode", ["train", "retrieval"])
+@pytest.mark.parametrize("mode", ["train", "retrieval", "evaluate"])
 def test_batch_bit_exact_vs_pil_torchvision(mode):
     rng = np.random.default_rng(7)
     imgs = [Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)) for h, w in SIZES]
@@ -38,3 +38,13 @@ def test_empty_and_errors():
         pre([np.zeros((10, 10), np.uint8)])
     with pytest.raises(ValueError):
         ImagePreprocessor("nope")
+
+
+def test_size_override_matches_square_resize():
+    """MisinformationPredictor with a 224 ViT: Resize((224, 224)) + ImageNet normalisation."""
+    rng = np.random.default_rng(9)
+    imgs = [Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)) for h, w in SIZES[:4]]
+    out = ImagePreprocessor("evaluate", size=224)(imgs).cpu().numpy()
+    c = MODES["evaluate"]
+    for i, im in enumerate(imgs):
+        assert np.array_equal(out[i], preprocess(im, (224, 224), None, c["mean"], c["std"]))
