@@ -15,6 +15,7 @@ import argparse
 import logging
 import os
 
+import numpy as np
 import torch
 
 from . import kernels as K
@@ -64,63 +65,95 @@ def category_loss(pred, labels):
 
 
 class FusionTrainer:
-    """Encoders + fusion head + AdamW as one training step."""
+    """Encoders + fusion head + AdamW as one training step (train.py:123-188).
+
+    Batches come in two forms (mmfd.dataset.stack_pairs): encoder inputs (input_ids /
+    attention_mask [2B, L] and pixel_values [2B, 3, S, S], claims first) or pre-computed encoder
+    outputs (claim_text_embeds / doc_text_embeds / claim_image_embeds / doc_image_embeds, the
+    reference's --pre_embed mode, train.py:127-132; the encoders may then be None). Each encoder
+    is frozen (eval, no grad: the reference's behaviour, train.py:335-340) or fine-tuned
+    (BASELINE config 3) on its own: freeze_text / freeze_image (default: freeze_encoders)."""
 
     def __init__(self, text_encoder, image_encoder, head, lr=1e-4, freeze_encoders=False, precision="bf16",
-                 dp=None):
+                 dp=None, freeze_text=None, freeze_image=None):
         self.text_encoder, self.image_encoder, self.head = text_encoder, image_encoder, head
-        self.freeze = freeze_encoders
+        self.freeze_text = freeze_encoders if freeze_text is None else bool(freeze_text)
+        self.freeze_image = freeze_encoders if freeze_image is None else bool(freeze_image)
+        self.freeze = self.freeze_text and self.freeze_image
         for m in (text_encoder, image_encoder, head):
-            m.set_precision(precision)
-        if freeze_encoders:
-            for m in (text_encoder, image_encoder):
+            if m is not None:
+                m.set_precision(precision)
+        trained = [head]
+        for m, frozen in ((text_encoder, self.freeze_text), (image_encoder, self.freeze_image)):
+            if m is None:
+                continue
+            if frozen:
                 m.eval()
                 for p in m.parameters():
                     p.requires_grad_(False)
-        params = list(head.parameters())
-        if not freeze_encoders:
-            params = list(text_encoder.parameters()) + list(image_encoder.parameters()) + params
-        self.params = params
-        self.optimizer = AdamW(params, lr=lr)
+            else:
+                trained.insert(len(trained) - 1, m)
+        self.params = [p for m in trained for p in m.parameters()]
+        self.optimizer = AdamW(self.params, lr=lr)
         self.dp = dp
         if dp is not None:
             # every replica starts from rank 0's weights (frozen encoders included: all ranks must
             # compute the same function), then the gradient all-reduce overlaps the backward pass
-            dp.broadcast_params([p for m in (text_encoder, image_encoder, head) for p in m.parameters()])
-            for m in ((head,) if freeze_encoders else (text_encoder, image_encoder, head)):
+            dp.broadcast_params([p for m in (text_encoder, image_encoder, head) if m is not None
+                                 for p in m.parameters()])
+            for m in trained:
                 m._grad_ready = dp.hook_for(m)
 
-    def step(self, batch):
-        self.optimizer.zero_grad(set_to_none=True)
+    def _device(self):
+        return next(self.head.parameters()).device
+
+    def features(self, batch):
+        """(X_t, X_i, E_t, E_i) for the head: the batch's pre-computed embeddings, or the encoders
+        on the stacked claim/evidence inputs (frozen ones without autograd)"""
+        dev = self._device()
+        if "claim_text_embeds" in batch:
+            return tuple(batch[k].to(dev, non_blocking=True) for k in
+                         ("claim_text_embeds", "claim_image_embeds", "doc_text_embeds", "doc_image_embeds"))
         B = batch["labels"].shape[0]
-        with torch.set_grad_enabled(not self.freeze):
-            T = self.text_encoder(input_ids=batch["input_ids"], attention_mask=batch["attention_mask"]).last_hidden_state
-            I = self.image_encoder(batch["pixel_values"]).last_hidden_state
-        outs = self.head(T[:B], I[:B], T[B:], I[B:])
-        loss = path_losses(outs, batch["labels"])
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
+            T = self.text_encoder(input_ids=batch["input_ids"].to(dev, non_blocking=True),
+                                  attention_mask=batch["attention_mask"].to(dev, non_blocking=True)).last_hidden_state
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_image):
+            I = self.image_encoder(batch["pixel_values"].to(dev, non_blocking=True)).last_hidden_state
+        return T[:B], I[:B], T[B:], I[B:]
+
+    def loss(self, outs, labels):
+        if self.head.factify or self.head.text_only:
+            return category_loss(outs[0], labels)
+        return path_losses(outs, labels)
+
+    def step(self, batch, return_outputs=False):
+        """one optimizer step; returns the device loss vector [total, tt, ti, it, ii] (and the
+        logits with return_outputs)"""
+        self.optimizer.zero_grad(set_to_none=True)
+        outs = self.head(*self.features(batch))
+        loss = self.loss(outs, batch["labels"].to(self._device(), non_blocking=True))
         if self.dp is not None:
             self.dp.begin()
         loss[0].backward()
         if self.dp is not None:
             self.dp.finish()
         self.optimizer.step()
-        return loss
-
+        return (loss, outs) if return_outputs else loss
 
     @torch.no_grad()
     def predict(self, batch):
         """Dual-encoder + fusion forward in eval mode (BASELINE config 2; the inference of
         evaluate.py:112-164 with batched pairs): ((y_tt, y_ti), (y_it, y_ii)) for claim =
-        batch[:B], evidence = batch[B:] of the stacked encoder inputs."""
-        mods = (self.text_encoder, self.image_encoder, self.head)
+        batch[:B], evidence = batch[B:] of the stacked encoder inputs (or the batch's embeddings)."""
+        mods = [m for m in (self.text_encoder, self.image_encoder, self.head) if m is not None]
         was = [m.training for m in mods]
         for m in mods:
             m.eval()
         try:
-            B = batch["pixel_values"].shape[0] // 2
-            T = self.text_encoder(input_ids=batch["input_ids"], attention_mask=batch["attention_mask"]).last_hidden_state
-            I = self.image_encoder(batch["pixel_values"]).last_hidden_state
-            return self.head(T[:B], I[:B], T[B:], I[B:])
+            if "labels" not in batch and "claim_text_embeds" not in batch:
+                batch = dict(batch, labels=torch.empty(batch["pixel_values"].shape[0] // 2))
+            return self.head(*self.features(batch))
         finally:
             for m, w in zip(mods, was):
                 m.train(w)
@@ -142,48 +175,248 @@ def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders
 
 
 def parse_args(argv=None):
-    """train.py:24-85 flag names, plus --precision / --synthetic / --steps."""
+    """train.py:24-85 (same flags and defaults), plus mmfd's: --precision, --image_encoder,
+    --synthetic, --steps, --init_checkpoint, --tokenizer, --world_size-free DP via torchrun."""
     ap = argparse.ArgumentParser(description="Train misinformation detection model (MI355X)")
-    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--epochs", type=int, default=50)
     ap.add_argument("--batch_size", type=int, default=32)
     ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--num_workers", type=int, default=8)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--embed_dim", type=int, default=256)
+    ap.add_argument("--num_heads", type=int, default=8)
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--hidden_dim", type=int, default=64)
+    ap.add_argument("--num_classes", type=int, default=3)
+    ap.add_argument("--mlp_ratio", type=float, default=4.0)
+    ap.add_argument("--fused_attn", action="store_true", help="accepted: eager and SDPA are one kernel here")
+    ap.add_argument("--train_data", type=str, default="./data/preprocessed/train.csv")
+    ap.add_argument("--val_data", type=str)
+    ap.add_argument("--text_encoder", type=str, default="microsoft/deberta-v3-xsmall",
+                    help="microsoft/deberta-v3-xsmall (frozen) or bert-base-uncased")
+    ap.add_argument("--output_dir", type=str, default="./results")
+    ap.add_argument("--save_every", type=int, default=2000)
+    ap.add_argument("--log_every", type=int, default=100)
+    ap.add_argument("--wandb_project", type=str, default="misinformation-detection", help="accepted; metrics go to "
+                    "<output_dir>/metrics.jsonl under the reference's wandb keys")
+    ap.add_argument("--wandb_entity", type=str, default=None)
     ap.add_argument("--freeze_text", action="store_true")
     ap.add_argument("--freeze_image", action="store_true")
-    ap.add_argument("--log_every", type=int, default=100)
-    ap.add_argument("--output_dir", type=str, default="./results")
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default="bf16")
-    ap.add_argument("--synthetic", type=int, default=1024, help="number of synthetic Factify-shaped pairs")
-    ap.add_argument("--steps", type=int, default=0, help="stop after N steps (0 = full epochs)")
+    ap.add_argument("--validate_every_epoch", action="store_true")
+    ap.add_argument("--save_best", action="store_true")
+    ap.add_argument("--best_metric", type=str, default="avg_f1",
+                    choices=["avg_f1", "avg_accuracy", "text_text_f1", "text_image_f1", "image_text_f1",
+                             "image_image_f1"])
+    ap.add_argument("--log_confusion_matrix", action="store_true")
+    ap.add_argument("--log_confusion_matrix_every", type=int, default=1000)
+    ap.add_argument("--pre_embed", action="store_true")
+    ap.add_argument("--text_input_dim", type=int, default=384)
+    ap.add_argument("--image_input_dim", type=int, default=1024)
+    # mmfd
+    ap.add_argument("--image_encoder", type=str, default="microsoft/swinv2-base-patch4-window8-256",
+                    help="microsoft/swinv2-base-patch4-window8-256 (frozen) or google/vit-base-patch16-224")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--synthetic", type=int, default=0,
+                    help="train on N synthetic Factify-shaped pairs instead of --train_data")
+    ap.add_argument("--steps", type=int, default=0, help="stop after N optimizer steps (0 = all epochs)")
+    ap.add_argument("--init_checkpoint", type=str, default=None, help="model_state_dict to start from")
+    ap.add_argument("--tokenizer", type=str, default=None, help="local HF tokenizer directory for raw text")
     return ap.parse_args(argv)
 
 
+TEXT_ENCODERS = ("microsoft/deberta-v3-xsmall", "bert-base-uncased")
+IMAGE_ENCODERS = ("microsoft/swinv2-base-patch4-window8-256", "google/vit-base-patch16-224")
+
+
+def build_encoders(args, device):
+    """the encoders of train.py:329-340 (random init: no hub download here). DeBERTa-v3 / Swinv2
+    are inference encoders in mmfd and therefore always frozen, as in the reference; bert-base /
+    ViT-B/16 train unless --freeze_text / --freeze_image."""
+    if args.text_encoder == "microsoft/deberta-v3-xsmall":
+        from .deberta import DebertaV2Config, DebertaV2Model
+        text, text_frozen = DebertaV2Model(DebertaV2Config()), True
+    elif args.text_encoder == "bert-base-uncased":
+        text, text_frozen = BertModel(BertConfig()), args.freeze_text
+    else:
+        raise ValueError(f"--text_encoder must be one of {TEXT_ENCODERS}")
+    if args.image_encoder == "microsoft/swinv2-base-patch4-window8-256":
+        from .swinv2 import Swinv2Config, Swinv2Model
+        image, image_frozen = Swinv2Model(Swinv2Config()), True
+    elif args.image_encoder == "google/vit-base-patch16-224":
+        image, image_frozen = ViTModel(ViTConfig()), args.freeze_image
+    else:
+        raise ValueError(f"--image_encoder must be one of {IMAGE_ENCODERS}")
+    return text.to(device), image.to(device), text_frozen, image_frozen
+
+
+def _metrics(preds, labels, prefix):
+    """train.py:191-214 / 296-303: accuracy, weighted F1 and per-class F1 per path (sklearn)"""
+    from sklearn.metrics import accuracy_score, f1_score
+    out = {}
+    for path in preds:
+        if not preds[path]:
+            continue
+        y, p = labels[path], preds[path]
+        out[f"{prefix}{path}_accuracy"] = float(accuracy_score(y, p))
+        out[f"{prefix}{path}_f1"] = float(f1_score(y, p, average="weighted"))
+        for i, f in enumerate(f1_score(y, p, average=None)):
+            out[f"{prefix}{path}_class{i}_f1"] = float(f)
+    return out
+
+
+def _collect(outs, labels, preds, labs, factify):
+    """host-side argmax of a step's logits (only at log time: no per-step device sync)"""
+    labels = labels.cpu()
+    if factify:
+        preds.setdefault("category", []).extend(outs[0].argmax(-1).cpu().tolist())
+        labs.setdefault("category", []).extend(labels.reshape(-1).tolist())
+        return
+    for idx, (path, y) in enumerate(zip(PATHS, (y for pr in outs for y in pr))):
+        if y is not None:
+            preds.setdefault(path, []).extend(y.argmax(-1).cpu().tolist())
+            labs.setdefault(path, []).extend(labels[:, idx].tolist())
+
+
+@torch.no_grad()
+def evaluate(trainer, loader):
+    """validation pass (the intent of train.py:248-309, whose model.tokenizer / raw-image inputs
+    cannot run): per-path mean loss + accuracy / F1"""
+    n, tot = 0, None
+    preds, labs = {}, {}
+    for batch in loader:
+        outs = trainer.predict(batch)
+        labels = batch["labels"].to(trainer._device())
+        loss = trainer.loss(outs, labels)
+        tot = loss if tot is None else tot + loss
+        n += 1
+        _collect(outs, labels, preds, labs, trainer.head.factify or trainer.head.text_only)
+    vals = (tot / max(n, 1)).tolist() if tot is not None else [0.0] * 5
+    return {p: v for p, v in zip(PATHS, vals[1:])}, _metrics(preds, labs, "")
+
+
+def _save(path, **state):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    torch.save(state, path)
+
+
 def main(args):
-    device = torch.device(f"cuda:{args.device}")
+    """train.py:311-434 on the HIP path"""
+    import functools
+    import json
+    import torch.distributed as dist
+    from torch.utils.data import DataLoader
+    from .dataset import MisinformationDataset, SyntheticFactifyDataset, get_dataloader, stack_pairs
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(args.device)))
+    device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
-    tr = build_flagship(device, args.precision, args.dropout, freeze_encoders=args.freeze_text and args.freeze_image,
-                        lr=args.lr, seed=args.seed)
+    dp = None
+    if world > 1:
+        from .dp import GradAllReduce
+        dist.init_process_group("nccl", device_id=device)
+        dp = GradAllReduce()
     os.makedirs(args.output_dir, exist_ok=True)
-    steps_per_epoch = max(1, args.synthetic // args.batch_size)
-    global_step = 0
+    torch.manual_seed(args.seed)  # set_seed (train.py:97-101)
+    text = image = None
+    ft = fi = True
+    if not args.pre_embed:
+        text, image, ft, fi = build_encoders(args, device)
+    head = MisinformationDetectionModel(text_input_dim=args.text_input_dim, image_input_dim=args.image_input_dim,
+                                        embed_dim=args.embed_dim, num_heads=args.num_heads, dropout=args.dropout,
+                                        hidden_dim=args.hidden_dim, num_classes=args.num_classes,
+                                        mlp_ratio=args.mlp_ratio, fused_attn=args.fused_attn)
+    if args.init_checkpoint:
+        ck = torch.load(args.init_checkpoint, map_location="cpu", weights_only=True)
+        head.load_state_dict(ck.get("model_state_dict", ck))
+    head = head.to(device)
+    head.manual_seed(args.seed + 7919 * rank)
+    if text is not None and hasattr(text, "manual_seed"):
+        text.manual_seed(args.seed + 1 + 7919 * rank)
+    tr = FusionTrainer(text, image, head, lr=args.lr, precision=args.precision, dp=dp, freeze_text=ft,
+                       freeze_image=fi)
+    tok = None
+    if args.tokenizer:
+        from transformers import AutoTokenizer
+        tok = AutoTokenizer.from_pretrained(args.tokenizer)
+    collate = functools.partial(stack_pairs, tokenizer=tok)
+    if args.synthetic:
+        size = 256 if "swinv2" in args.image_encoder else 224
+        ds = SyntheticFactifyDataset(args.synthetic, seq_len=128, image_size=size, seed=args.seed, ragged=True)
+        workers = 0
+    else:
+        ds = MisinformationDataset(args.train_data, pre_embed=args.pre_embed)
+        workers = args.num_workers
+    # data parallel: each rank draws its own shard of every epoch (DistributedSampler)
+    sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed) \
+        if world > 1 else None
+    loader = DataLoader(ds, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
+                        num_workers=workers, pin_memory=True, collate_fn=collate)
+    val_loader = None
+    if args.validate_every_epoch:
+        if not args.val_data:
+            raise ValueError("--val_data must be specified when --validate_every_epoch is set")
+        val_loader = get_dataloader(args.val_data, batch_size=args.batch_size, shuffle=False,
+                                    num_workers=args.num_workers, pre_embed=args.pre_embed, collate_fn=collate)
+    log = open(os.path.join(args.output_dir, "metrics.jsonl"), "a") if rank == 0 else None
+    global_step, best = 0, float("-inf")
+    single = tr.head.factify or tr.head.text_only  # train.py always builds the 4-path head
     for epoch in range(args.epochs):
-        for s in range(steps_per_epoch):
-            batch = synthetic_batch(args.batch_size, seed=args.seed * 100003 + global_step, device=device)
-            loss = tr.step(batch)
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        preds, labs, pending = {}, {}, []
+        for batch in loader:
+            loss, outs = tr.step(batch, return_outputs=True)
+            pending.append((loss.detach(), outs, batch["labels"]))
             if global_step % args.log_every == 0:
+                for _, o_, y_ in pending:
+                    _collect(o_, y_, preds, labs, single)
                 vals = loss.tolist()
-                logger.info("epoch %d step %d total_loss %.4f %s", epoch, global_step, vals[0],
-                            " ".join(f"{n}={v:.4f}" for n, v in zip(PATHS, vals[1:])))
+                rec = {"train/total_loss": vals[0], **{f"train/{p}_loss": v for p, v in zip(PATHS, vals[1:])},
+                       "train/learning_rate": args.lr, "train/step": global_step, "epoch": epoch,
+                       **_metrics(preds, labs, "train/")}
+                logger.info("epoch %d step %d total_loss %.4f", epoch, global_step, vals[0])
+                if log:
+                    log.write(json.dumps(rec) + "\n")
+                    log.flush()
+                preds, labs = {}, {}
+                pending = []
+            elif len(pending) > args.log_every:
+                pending = pending[-args.log_every:]
+            if global_step % args.save_every == 0 and rank == 0:  # train.py:234-242
+                _save(os.path.join(args.output_dir, f"checkpoint-{epoch}-{global_step}", "model.pt"),
+                      global_step=global_step, epoch=epoch, model_state_dict=tr.head.state_dict(),
+                      optimizer_state_dict=tr.optimizer.state_dict())
             global_step += 1
             if args.steps and global_step >= args.steps:
                 break
-        torch.save({"global_step": global_step, "epoch": epoch, "model_state_dict": tr.head.state_dict(),
-                    "optimizer_state_dict": tr.optimizer.state_dict()},
-                   os.path.join(args.output_dir, f"checkpoint-{epoch}-{global_step}.pt"))
+        if val_loader is not None:
+            vl, vm = evaluate(tr, val_loader)
+            if log:
+                log.write(json.dumps({"val/loss": sum(vl.values()) / len(vl), **{f"val/{k}_loss": v for k, v in vl.items()},
+                                      **{f"val/{k}": v for k, v in vm.items()}, "epoch": epoch,
+                                      "global_step": global_step}) + "\n")
+            if args.save_best and rank == 0:  # train.py:409-428
+                if args.best_metric == "avg_f1":
+                    cur = float(np.mean([v for k, v in vm.items() if k.endswith("_f1") and "class" not in k]))
+                elif args.best_metric == "avg_accuracy":
+                    cur = float(np.mean([v for k, v in vm.items() if "accuracy" in k]))
+                else:
+                    cur = vm.get(args.best_metric)
+                if cur is not None and cur > best:
+                    best = cur
+                    _save(os.path.join(args.output_dir, "best_model.pt"), epoch=epoch, global_step=global_step,
+                          model_state_dict=tr.head.state_dict(), optimizer_state_dict=tr.optimizer.state_dict(),
+                          **{args.best_metric: best})
         if args.steps and global_step >= args.steps:
             break
+    if log:
+        log.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return tr, global_step
 
 
 if __name__ == "__main__":  # pragma: no cover

@@ -166,3 +166,52 @@ def test_cached_weights_invalidate_on_load_state_dict_and_data_writes():
     Bk.shadow_store(m)["k"] = (torch.zeros(1), [])
     m.float()
     assert not Bk.shadow_store(m)
+
+
+def test_cli_flags_mirror_reference_defaults():
+    """train.py:24-85: same flag names and defaults (mmfd's additions listed separately)."""
+    from mmfd.train import parse_args
+    a = parse_args([])
+    want = dict(epochs=50, batch_size=32, lr=1e-4, num_workers=8, device=0, seed=42, embed_dim=256, num_heads=8,
+                dropout=0.1, hidden_dim=64, num_classes=3, mlp_ratio=4.0, fused_attn=False,
+                train_data="./data/preprocessed/train.csv", val_data=None, text_encoder="microsoft/deberta-v3-xsmall",
+                output_dir="./results", save_every=2000, log_every=100, wandb_project="misinformation-detection",
+                wandb_entity=None, freeze_text=False, freeze_image=False, validate_every_epoch=False, save_best=False,
+                best_metric="avg_f1", log_confusion_matrix=False, log_confusion_matrix_every=1000, pre_embed=False,
+                text_input_dim=384, image_input_dim=1024)
+    for k, v in want.items():
+        assert getattr(a, k) == v, k
+    b = parse_args(["--pre_embed", "--freeze_text", "--text_input_dim", "768", "--save_every", "5"])
+    assert b.pre_embed and b.freeze_text and not b.freeze_image and b.text_input_dim == 768 and b.save_every == 5
+
+
+def test_stack_pairs_collates_every_item_kind():
+    from mmfd.dataset import SyntheticFactifyDataset, stack_pairs
+    ds = SyntheticFactifyDataset(3, seq_len=20, image_size=16, ragged=True)
+    b = stack_pairs([ds[i] for i in range(3)])
+    assert b["input_ids"].shape == (6, 20) and b["pixel_values"].shape == (6, 3, 16, 16) and b["labels"].shape == (3, 4)
+    assert torch.equal(b["input_ids"][0], ds[0]["claim_input_ids"]) and torch.equal(b["input_ids"][3], ds[0]["document_input_ids"])
+    emb = [{"id": str(i), "claim_text_embeds": torch.zeros(5, 4), "doc_text_embeds": torch.zeros(5, 4),
+            "claim_image_embeds": torch.zeros(3, 6), "doc_image_embeds": torch.zeros(3, 6),
+            "labels": torch.tensor([0, 1, 1, 1])} for i in range(2)]
+    e = stack_pairs(emb)
+    assert e["claim_text_embeds"].shape == (2, 5, 4) and e["labels"].shape == (2, 4)
+    with pytest.raises(ValueError):
+        stack_pairs([{"id": "0", "claim": "a", "document": "b", "claim_image": torch.zeros(3, 4, 4),
+                      "document_image": torch.zeros(3, 4, 4), "labels": torch.zeros(4, dtype=torch.long)}])
+
+
+def test_misinformation_dataset_reads_npz_store(tmp_path):
+    import numpy as np
+    from mmfd.dataset import MisinformationDataset, get_dataloader
+    d = tmp_path / "train_embeddings"
+    d.mkdir()
+    for i in range(3):
+        np.savez(d / f"{i}.npz", claim_text_embeds=np.full((4, 2), i, np.float32), doc_text_embeds=np.zeros((4, 2), np.float32),
+                 claim_image_embeds=np.zeros((3, 5), np.float32), doc_image_embeds=np.zeros((3, 5), np.float32),
+                 labels=np.array([0, 1, 1, 1]))
+    ds = MisinformationDataset(str(tmp_path / "train.csv"), pre_embed=True)
+    assert len(ds) == 3 and ds[2]["claim_text_embeds"][0, 0].item() == 2.0 and ds[1]["id"] == "1"
+    assert next(iter(get_dataloader(str(tmp_path / "train.csv"), batch_size=3, num_workers=0, pre_embed=True)))["labels"].shape == (3, 4)
+    with pytest.raises(FileNotFoundError):
+        MisinformationDataset(str(tmp_path / "missing.csv"), pre_embed=True)
