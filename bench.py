@@ -601,6 +601,7 @@ def main():
                                                   "preembed", "preembed_image"],
                     default="train")
     ap.add_argument("--no-bf16", action="store_true", help="skip the secondary bf16 leg of the fp32 headline")
+    ap.add_argument("--graph", action="store_true", help="time HIP-graph replays of the captured step (experimental)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -654,11 +655,11 @@ def main():
                        "bert-base-uncased + ViT-B/16 + fusion head (768/768, E=256, H=8), fwd+bwd+AdamW",
                        "global_batch": args.batch * world, "seq_len": 128, "image_size": 224,
                        "parallelism": f"dp{world}"},
-            "roofline": res["roofline"],
+            "roofline": res["roofline"], "step_launch": res["launch"],
             "step_tflops_per_gpu": round(res["step_tflops"], 1),
             "step_mfma_frac": round(res["step_tflops"] / peak, 4),
             "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
-            "final_loss": res["loss"],
+            "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"],
         }
         if sec is not None:
             out["bf16"] = {"value": round(sec["pairs"], 2), "unit": "pairs/s", "ms_per_step": round(sec["ms"], 3),
@@ -689,17 +690,27 @@ def train_leg(args, dev, world, rank, precision):
     tr = build_flagship(dev, precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42, rank=rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 
-    for _ in range(args.warmup):
-        tr.step(batch)
+    graphed = world == 1 and args.graph
+    probe = K.GemmProbe()
+    if graphed:  # the whole step as one HIP graph (capture runs its own eager warmup steps first)
+        tr.capture(batch, warmup=max(1, args.warmup))
+        for _ in range(args.warmup):
+            tr.replay()
+    else:
+        for _ in range(args.warmup):
+            tr.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    probe = K.GemmProbe()
     t0 = time.perf_counter()
-    with probe:
+    if graphed:
         for _ in range(args.steps):
-            loss = tr.step(batch)
+            loss = tr.replay()
+    else:
+        with probe:
+            for _ in range(args.steps):
+                loss = tr.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -713,20 +724,35 @@ def train_leg(args, dev, world, rank, precision):
     pairs = args.batch * world * args.steps / elapsed
     loss_val = loss[0].item()
 
-    prof = probe.summary()
+    if graphed:
+        # per-GEMM device times: events cannot be timed inside a graph, so two more steps of the
+        # same trainer run eagerly with the probe (the same kernels on the same shapes)
+        steps_in_prof = 2
+        with probe:
+            for _ in range(steps_in_prof):
+                tr.step(batch)
+        prof = probe.summary()
+    else:
+        prof = probe.summary()
+        steps_in_prof = args.steps
     dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[precision]
-    gemm_ms = sum(v["ms"] for v in prof.values()) / args.steps
+    gemm_ms = sum(v["ms"] for v in prof.values()) / steps_in_prof
     gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(dom_name)
+    kinds = {k: {"launches_per_step": v["launches"] // steps_in_prof, "avg_us": round(1000.0 * v["ms"] / v["launches"], 1),
+                 "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
+             for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
     del tr, batch
-    return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2),
+    return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
+            "launch": ("one HIP graph per step (captured fwd + bwd + AdamW); GEMM times from 2 eager probe steps "
+                       "after the timed replays") if graphed else "eager kernel launches (GEMM times over the timed steps)",
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
             "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                         "launches_per_step": d["launches"] // args.steps,
+                         "launches_per_step": d["launches"] // steps_in_prof,
                          "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
                          "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])}}
 

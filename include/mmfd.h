@@ -35,7 +35,9 @@ enum {
   MMFD_ACT_GELU = 1,      /* exact erf GELU, nn.GELU() (layers.py:14) / HF "gelu" */
   MMFD_ACT_RELU = 2,      /* nn.ReLU() (model.py:264 ...) */
   MMFD_ACT_GELU_BWD = 3,  /* out *= gelu'(aux)  (aux = saved pre-activation) */
-  MMFD_ACT_RELU_BWD = 4   /* out *= (aux > 0)   */
+  MMFD_ACT_RELU_BWD = 4,  /* out *= (aux > 0)   */
+  MMFD_ACT_TANH = 5,      /* tanh (HF BertPooler, the cross-encoder's [CLS] pooler), forward only */
+  MMFD_ACT_SIGMOID = 6    /* 1 / (1 + exp(-x)) (CrossEncoder's default score activation) */
 };
 enum { MMFD_OK = 0, MMFD_ERR_INVALID = 1000, MMFD_ERR_UNSUPPORTED = 1001 };
 
@@ -316,6 +318,9 @@ int mmfd_adamw(int n_tensors, const mmfd_adamw_tensor* table, int64_t max_numel,
 /* ------------------------------------------------------------------------------------------- */
 /* out(dtype_out) = in(dtype_in) * scale (+ add) — casts / scaled copies / grad accumulation. */
 int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream);
+/* dst[0 .. bytes) = 0 on the stream, by a kernel (graph-capture safe); the scatter-add targets of
+   the embedding backward */
+int mmfd_zero(void* dst, int64_t bytes, mmfd_stream_t stream);
 int mmfd_axpby(int dtype, int64_t n, float a, const void* x, float b, const void* y, void* out,
                mmfd_stream_t stream);
 /* generic dropout (out = keep ? x/(1-p) : 0), index = element index. */

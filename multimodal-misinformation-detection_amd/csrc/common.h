@@ -73,6 +73,11 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
+// forward-only epilogue activations past ReLU (MMFD_ACT_TANH / MMFD_ACT_SIGMOID)
+__device__ __forceinline__ float act_tail_f(int act, float z) {
+  return act == MMFD_ACT_TANH ? tanhf(z) : 1.0f / (1.0f + expf(-z));
+}
+
 // ---------------------------------------------------------------------------------------------
 // counter-based dropout RNG: keep(element) is a pure function of (seed, salt, index), so the
 // backward pass regenerates the forward mask and the CPU oracle can reproduce it bit-for-bit.

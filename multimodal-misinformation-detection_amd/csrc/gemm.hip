@@ -55,6 +55,8 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
     z *= gelu_grad_f(to_f32(reinterpret_cast<const TC*>(e.aux)[row * e.ldaux + col]));
   } else if (e.act == MMFD_ACT_RELU_BWD) {
     z = (to_f32(reinterpret_cast<const TC*>(e.aux)[row * e.ldaux + col]) > 0.0f) ? z : 0.0f;
+  } else if (e.act >= MMFD_ACT_TANH) {
+    z = act_tail_f(e.act, z);
   }
   if (e.p > 0.0f) {
     const uint32_t h = mmfd_hash_k(hkey, (uint64_t)row * (uint64_t)N + (uint64_t)col);
@@ -145,6 +147,9 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
 #pragma unroll
       for (int q = 0; q < 8; ++q) z[q] = a[q] > 0.0f ? z[q] : 0.0f;
     }
+  } else if (e.act >= MMFD_ACT_TANH) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] = act_tail_f(e.act, z[q]);
   }
   if (e.p > 0.0f) {
     const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)col;
@@ -172,7 +177,7 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
 // chunk c of row r at chunk c ^ (r & 7) (conflict-free ds_read_b128 fragments). Layout 1
 // ("MN-contiguous": A[k][m] / B[k][n]): [BK rows][MNW elements]; bf16 fragments come from
 // ds_read_b64_tr_b16 with 8-B unit u of row r at u ^ 4*((r&3) | ((r>>3)&1)<<2) (conflict-free tr
-// reads), fp32 fragments from 4 ds_read_b32 with chunk c at c ^ 4*((r>>2)&1).
+// reads), fp32 fragments from 4 ds_read_b32 with chunk c at c ^ 4*((r>>2)&3) (see swz).
 // -------------------------------------------------------------------------------------------------
 // SW = 1 (layout 0 only): the B image of the 256x256 kernel, whose fragments gather rows
 // 8p + 4j + (0..3) (see g8_load_b); chunk c of row r at c ^ (2*((r>>1)&1) | 4*((r>>3)&1)) keeps
@@ -186,7 +191,12 @@ struct Img {
     if (LAYOUT == 0 && SW == 1) return c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2));
     if (LAYOUT == 0) return c ^ (r & 7);
     if (sizeof(T) == 2) return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
-    return c ^ (4 * ((r >> 2) & 1));
+    // fp32, MN-contiguous: a fragment is 4 ds_read_b32 whose 16-lane groups g read rows 4g + s (the
+    // rows of a group are 4 * 128 or 256 dwords apart = the same banks). A-type fragments read 4
+    // consecutive chunks per group: XOR by 4 * g puts the groups on disjoint banks. The G8 B image
+    // (SW = 1) is read as chunks {b, b+2, b+4, b+6}: XOR by {0, 1, 8, 9} separates those.
+    if (SW == 1) return c ^ (((r >> 2) & 1) | (((r >> 3) & 1) << 3));
+    return c ^ (4 * ((r >> 2) & 3));
   }
 };
 
@@ -399,8 +409,9 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 }
 
 // =================================================================================================
-// bf16 256x256 kernel ("G8"): 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns four 64x32 quadrants
-// (mq, nq): rows mq*128 + wr*64 + [0,64), cols nq*128 + wc*32 + [0,32). Each K-tile (64 bf16) is
+// 256x256 kernel ("G8", bf16 and fp32 operands): 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns four
+// 64x32 quadrants (mq, nq): rows mq*128 + wr*64 + [0,64), cols nq*128 + wc*32 + [0,32). Each K-tile
+// (128 B of K per row: 64 bf16 / 32 fp32) is
 // staged as four 16-KB half-tiles (A rows [0,128) / [128,256), B cols [0,128) / [128,256)) into
 // one of two LDS buffers by LDS-DMA, and consumed in four phases, one quadrant (16 MFMAs) each:
 //   phase 0: (0,0) reads A-h0, B-h0   phase 1: (0,1) reads B-h1
@@ -412,7 +423,8 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 // =================================================================================================
 constexpr int G8_HALF = 16384;
 constexpr int G8_LDS = 128 * (256 + 4) * 4;  // >= 2 buffers x 4 half-tiles (128 KB); 128-row epilogue staging
-constexpr int G8_BM = 256, G8_BN = 256, G8_BK = 64;
+constexpr int G8_BM = 256, G8_BN = 256;
+template <typename T> struct G8T { static constexpr int BK = ROWB / (int)sizeof(T); };  // K per K-tile
 
 __device__ __forceinline__ void g8_pre_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS reads retired (WAR vs the next refill)
@@ -425,12 +437,12 @@ __device__ __forceinline__ void g8_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int LAYOUT>
+template <typename T, int LAYOUT>
 __device__ __forceinline__ void g8_frag_a(uint4 (&a)[4][2], const char* img, int wr, int lane) {
 #pragma unroll
   for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<bf16, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
+    for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<T, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
 }
 // B fragment j (j = 0, 1) of the wave's 32 columns gathers the 4-column units 2p + j (p = 0..3),
 // and the MFMA runs with swapped operands (acc = B-fragment x A-fragment = the C^T block): lane
@@ -439,29 +451,41 @@ __device__ __forceinline__ void g8_frag_a(uint4 (&a)[4][2], const char* img, int
 // register epilogue. The K-contiguous B image uses the SW = 1 swizzle under which these
 // ds_read_b128 are conflict-free; the MN-contiguous (transposed ds_read_b64_tr_b16) B reads are
 // 2-way (each 16-B chunk is read in one half only), well inside the LDS budget of a K-tile.
-template <int LAYOUT>
+// fp32 operands: the same column interleave, the 16x16x4 fragment being 4 consecutive k of the
+// row (layout 0: one ds_read_b128; layout 1: 4 ds_read_b32 down the K rows of the column)
+template <typename T, int LAYOUT>
 __device__ __forceinline__ uint4 g8_load_b(const char* img, int wc, int j, int kc, int lane) {
-  using I = Img<bf16, LAYOUT, 128, 1>;
+  using I = Img<T, LAYOUT, 128, 1>;
   const int g = lane >> 4, i = lane & 15;
   if (LAYOUT == 0) {
     const int row = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
     return lds_read16(img, row * ROWB + (I::swz(row, kc * 4 + g) << 4));
-  } else {
+  } else if (sizeof(T) == 2) {
     const int q = i >> 2, p = i & 3;
     const int r1 = kc * 32 + 8 * g + q, r2 = r1 + 4;
     const int u = wc * 8 + 2 * p + j;  // 8-B unit (4 bf16)
     const uint2 a = lds_read_tr16(img + r1 * I::RBY + (I::swz(r1, u >> 1) << 4) + ((u & 1) << 3));
     const uint2 b = lds_read_tr16(img + r2 * I::RBY + (I::swz(r2, u >> 1) << 4) + ((u & 1) << 3));
     return make_uint4(a.x, a.y, b.x, b.y);
+  } else {
+    const int col = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
+    uint32_t v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = kc * 16 + 4 * g + s;
+      v[s] = *reinterpret_cast<const uint32_t*>(img + row * I::RBY + (I::swz(row, col >> 2) << 4) + (col & 3) * 4);
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
   }
 }
-template <int LAYOUT>
+template <typename T, int LAYOUT>
 __device__ __forceinline__ void g8_frag_b(uint4 (&b)[2][2], const char* img, int wc, int lane) {
 #pragma unroll
   for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j][kc] = g8_load_b<LAYOUT>(img, wc, j, kc, lane);
+    for (int j = 0; j < 2; ++j) b[j][kc] = g8_load_b<T, LAYOUT>(img, wc, j, kc, lane);
 }
+template <typename T>
 __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2], const uint4 (&b)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -469,11 +493,14 @@ __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) Mma<bf16>::run(acc[i][j], b[j][kc], a[i][kc]);
+      for (int j = 0; j < 2; ++j) Mma<T>::run(acc[i][j], b[j][kc], a[i][kc]);
   __builtin_amdgcn_s_setprio(0);
 }
 
-__device__ __forceinline__ float g8_sum8(uint4 x) {
+template <typename T>
+__device__ __forceinline__ float g8_sum16b(uint4 x) {  // the elements of one 16-B chunk
+  if (sizeof(T) == 4)
+    return (__uint_as_float(x.x) + __uint_as_float(x.y)) + (__uint_as_float(x.z) + __uint_as_float(x.w));
   return ((__uint_as_float(x.x << 16) + __uint_as_float(x.x & 0xffff0000u)) +
           (__uint_as_float(x.y << 16) + __uint_as_float(x.y & 0xffff0000u))) +
          ((__uint_as_float(x.z << 16) + __uint_as_float(x.z & 0xffff0000u)) +
@@ -481,10 +508,10 @@ __device__ __forceinline__ float g8_sum8(uint4 x) {
 }
 // wave wc sums A subtile wc of the half-tile (its own two LDS reads: a runtime subtile index into
 // the fragment registers would push them to scratch)
-template <int LAYOUT>
+template <typename T, int LAYOUT>
 __device__ __forceinline__ float g8_rowsum(const char* img, int wr, int wc, int lane) {
-  return g8_sum8(load_frag<bf16, LAYOUT, 128>(img, wr * 4 + wc, 0, lane)) +
-         g8_sum8(load_frag<bf16, LAYOUT, 128>(img, wr * 4 + wc, 1, lane));
+  return g8_sum16b<T>(load_frag<T, LAYOUT, 128>(img, wr * 4 + wc, 0, lane)) +
+         g8_sum16b<T>(load_frag<T, LAYOUT, 128>(img, wr * 4 + wc, 1, lane));
 }
 
 // Diagnostic build only (-DMMFD_G8_STAMPS, tools/g8_stamps.py): per-wave s_memtime stamps at
@@ -504,9 +531,9 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 
 // PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
 // prefetched for all of a thread's rows before the accumulators are staged (see the epilogue)
-template <int TA, int TB, typename TC, bool PRE>
+template <typename T, int TA, int TB, typename TC, bool PRE>
 __global__ void __launch_bounds__(NT, 1)
-gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
                float alpha, int tiles_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
                int rs_mode) {
@@ -518,6 +545,8 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   const int gx = gridDim.x, gy = gridDim.y;
   const int tile = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   const int64_t m0 = (int64_t)(tile / gx) * G8_BM, n0 = (int64_t)(tile % gx) * G8_BN;
+  constexpr int G8_BK = G8T<T>::BK;
+  constexpr int64_t ESZ = sizeof(T);
   const int nkt_total = (int)((K + G8_BK - 1) / G8_BK);
   const int kt0 = blockIdx.z * tiles_per_split;
   const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
@@ -532,10 +561,10 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * 2);
-  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * 2);
-  Fill<bf16, TA, 128, 2> fa0, fa1;
-  Fill<bf16, TB, 128, 2, 1> fb0, fb1;
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * ESZ);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * ESZ);
+  Fill<T, TA, 128, 2> fa0, fa1;
+  Fill<T, TB, 128, 2, 1> fb0, fb1;
   fa0.init(lda, m0, M, wave, lane);
   fa1.init(lda, m0 + 128, M, wave, lane);
   fb0.init(ldb, n0, N, wave, lane);
@@ -547,11 +576,11 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     const int64_t k0 = (int64_t)(kt0 + t) * G8_BK;
     const bool tail = k0 + G8_BK > K;
     if (h < 2) {
-      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * 2);
+      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * ESZ);
       if (h == 0) fa0.issue(rsa, img(t, 0), so, tail, k0, K, wave, lane);
       else fa1.issue(rsa, img(t, 1), so, tail, k0, K, wave, lane);
     } else {
-      const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * 2);
+      const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * ESZ);
       if (h == 2) fb0.issue(rsb, img(t, 2), so, tail, k0, K, wave, lane);
       else fb1.issue(rsb, img(t, 3), so, tail, k0, K, wave, lane);
     }
@@ -577,28 +606,28 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
   uint4 fa[4][2], fb[2][2];
   for (int t = 0; t < nk; ++t) {
     // phase 0: quadrant (0,0)
-    g8_frag_a<TA>(fa, img(t, 0), wr, lane);
-    g8_frag_b<TB>(fb, img(t, 2), wc, lane);
-    if (do_rs) rs0 += g8_rowsum<TA>(img(t, 0), wr, wc, lane);
+    g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
+    g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
+    if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
     if (t + 1 < nk) issue(2, t + 1);
     g8_pre_barrier();
-    g8_mma(acc[0][0], fa, fb);
+    g8_mma<T>(acc[0][0], fa, fb);
     g8_barrier();
     // phase 1: quadrant (0,1)
-    g8_frag_b<TB>(fb, img(t, 3), wc, lane);
+    g8_frag_b<T, TB>(fb, img(t, 3), wc, lane);
     if (t + 2 < nk) issue(0, t + 2);
     g8_pre_barrier();
-    g8_mma(acc[0][1], fa, fb);
+    g8_mma<T>(acc[0][1], fa, fb);
     g8_barrier();
     // phase 2: quadrant (1,1)
-    g8_frag_a<TA>(fa, img(t, 1), wr, lane);
-    if (do_rs) rs1 += g8_rowsum<TA>(img(t, 1), wr, wc, lane);
+    g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
+    if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
     if (t + 2 < nk) issue(3, t + 2);
     g8_pre_barrier();
-    g8_mma(acc[1][1], fa, fb);
+    g8_mma<T>(acc[1][1], fa, fb);
     g8_barrier();
     // phase 3: quadrant (1,0); K-tile t+1 must have landed before the next phase reads it
-    g8_frag_b<TB>(fb, img(t, 2), wc, lane);
+    g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
     if (t + 2 < nk) {
       issue(1, t + 2);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -606,7 +635,7 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     g8_pre_barrier();
-    g8_mma(acc[1][0], fa, fb);
+    g8_mma<T>(acc[1][0], fa, fb);
     g8_barrier();
   }
   G8_STAMP(1);
@@ -628,17 +657,6 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
     }
   }
 
-  if (alpha == 12345.0f) {  // EXPERIMENT: skip the epilogue (keep the accumulators alive)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
-    return;
-  }
   // ---- epilogue: two passes of 128 rows (quadrant row mq = pass); every wave stages its fp32
   // accumulators, then all threads apply the epilogue to 8-column chunks with 16-B accesses
   constexpr int LDC = G8_BN + 4;
@@ -721,6 +739,9 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
 #pragma unroll
               for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
             }
+          } else if (e.act >= MMFD_ACT_TANH) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = act_tail_f(e.act, z[u]);
           }
           if (e.p > 0.f) {
             const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
@@ -809,6 +830,9 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
 #pragma unroll
               for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
             }
+          } else if (e.act >= MMFD_ACT_TANH) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = act_tail_f(e.act, z[u]);
           }
           if (e.p > 0.f) {
             const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
@@ -824,11 +848,6 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
             rc[k].get(t);
 #pragma unroll
             for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
-          }
-          if (alpha == 23456.0f) {  // EXPERIMENT: everything but the global stores
-#pragma unroll
-            for (int u = 0; u < 8; ++u) asm volatile("" ::"v"(z[u]));
-            continue;
           }
           V8<TC>::store(cp + kk * cs, z);
         }
@@ -867,10 +886,6 @@ gemm256_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__
       float vv[8] = {alpha * a4.x, alpha * a4.y, alpha * a4.z, alpha * a4.w,
                      alpha * b4.x, alpha * b4.y, alpha * b4.z, alpha * b4.w};
       const bool full = col + 8 <= N;
-      if (alpha == 23456.0f) {  // EXPERIMENT: staging only, no global stores
-        asm volatile("" ::"v"(vv[0]), "v"(vv[3]), "v"(vv[7]));
-        continue;
-      }
       if (slab) {
         if (full && (N % 4) == 0) {
           *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -959,48 +974,53 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
                      a.alpha, tps, e);
 }
 
-template <int TA, int TB, typename TC, bool PRE>
+template <typename T, int TA, int TB, typename TC, bool PRE>
 void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
                  int rs_mode, hipStream_t s) {
   dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<TA, TB, TC, PRE>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<T, TA, TB, TC, PRE>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm256_kernel<TA, TB, TC, PRE>), grid, dim3(NT), G8_LDS, s, (const bf16*)a.A, a.lda,
-                     (const bf16*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
+  hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE>), grid, dim3(NT), G8_LDS, s, (const T*)a.A, a.lda,
+                     (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
                      a.a_rowsum_beta, rs_mode);
 }
 
-template <int TA, int TB, typename TC>
+template <typename T, int TA, int TB, typename TC>
 void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
                int rs_mode, hipStream_t s) {
   const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
   const int streams = (e.residual ? 1 : 0) + (bwd_act ? 1 : 0) + (e.beta != 0.f ? 1 : 0);
   if constexpr (std::is_same<TC, bf16>::value) {
-    if (streams == 1 && !ws && e.vec) return launch_g8_v<TA, TB, TC, true>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+    if (streams == 1 && !ws && e.vec) return launch_g8_v<T, TA, TB, TC, true>(a, e, ws, splits, tps, rs_out, rs_mode, s);
   }
-  launch_g8_v<TA, TB, TC, false>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  launch_g8_v<T, TA, TB, TC, false>(a, e, ws, splits, tps, rs_out, rs_mode, s);
 }
 
-template <typename TC>
+template <typename T, typename TC>
 void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
                  int rs_mode, hipStream_t s) {
-  if (!a.trans_a && !a.trans_b) launch_g8<0, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else if (!a.trans_a && a.trans_b) launch_g8<0, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else if (a.trans_a && !a.trans_b) launch_g8<1, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else launch_g8<1, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  if (!a.trans_a && !a.trans_b) launch_g8<T, 0, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else if (!a.trans_a && a.trans_b) launch_g8<T, 0, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else if (a.trans_a && !a.trans_b) launch_g8<T, 1, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  else launch_g8<T, 1, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
 }
 
 bool use_g8(const mmfd_gemm_args& a) {
   static const bool off = getenv("MMFD_GEMM_V1") != nullptr;
+  static const bool off_f32 = getenv("MMFD_GEMM_F32_V1") != nullptr;
   static const bool narrow_g8 = getenv("MMFD_GEMM_NARROW_G8") != nullptr;
   // tall GEMMs with N <= 128 or K < 64 (Swinv2 stage-1 out-projection / FFN2 at N = 128, its 4x4
   // patch embedding at K = 48): the 256x256 tile is half padding / all prologue, and the 256x128
   // kernel measured 20-35 % faster per launch (45 vs 66 us, 85 vs 107 us, 36 vs 55 us)
   if (!narrow_g8 && a.M >= 4096 && (a.N <= 128 || a.K < 64)) return false;
-  return a.dtype == MMFD_BF16 && !off;
+  if (off) return false;
+  if (a.dtype == MMFD_BF16) return true;
+  // fp32 operands (the parity / headline mode): the 256x256 tile halves the B-panel traffic per
+  // MFMA of the 256x128 kernel; fp32 C only (a bf16 C from fp32 operands stays on the 256x128 kernel)
+  return a.dtype == MMFD_F32 && a.c_dtype == MMFD_F32 && !off_f32;
 }
 
 template <typename T, typename TC>
@@ -1040,10 +1060,11 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
       // overhead) + the fp32 slab round trip (written by the blocks, read by the reduce) at ~5 TB/s
       double best = 1e30;
       const int smax = (int)std::min<int64_t>(32, nkt / 8);
+      const double kt_us = a.dtype == MMFD_BF16 ? 1.8 : 7.0;  // one 256x256 K-tile (bf16 / fp32 MFMA rate)
       for (int sp = 1; sp <= smax; ++sp) {
         const double rounds = (double)((tiles * sp + 255) / 256);
         const double kts = (double)((nkt + sp - 1) / sp);
-        double cost = rounds * (kts * 1.8 + 3.0);
+        double cost = rounds * (kts * kt_us + 3.0);
         if (sp > 1) cost += (double)sp * a.M * a.N * 8.0 / 5.0e6 + 4.0;
         if (cost < best) { best = cost; splits = sp; }
       }
@@ -1105,8 +1126,9 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   MMFD_CHECK_ARG(a.C != nullptr, "mmfd_gemm: null C");
   MMFD_CHECK_ARG(a.ldc >= a.N, "mmfd_gemm: ldc %lld < N %lld", (long long)a.ldc, (long long)a.N);
   const int act = a.ep.act;
-  MMFD_CHECK_ARG(act >= 0 && act <= 4, "mmfd_gemm: bad act %d", act);
-  MMFD_CHECK_ARG(!(act >= MMFD_ACT_GELU_BWD) || a.ep.aux != nullptr, "mmfd_gemm: backward act needs aux");
+  MMFD_CHECK_ARG(act >= 0 && act <= MMFD_ACT_SIGMOID, "mmfd_gemm: bad act %d", act);
+  MMFD_CHECK_ARG(!(act == MMFD_ACT_GELU_BWD || act == MMFD_ACT_RELU_BWD) || a.ep.aux != nullptr,
+                 "mmfd_gemm: backward act needs aux");
   MMFD_CHECK_ARG(a.ep.dropout_p <= 0.f || a.ep.seed != nullptr, "mmfd_gemm: dropout needs seed");
   MMFD_CHECK_ARG(a.ep.dropout_p < 1.f, "mmfd_gemm: dropout p must be < 1");
   if (a.M == 0 || a.N == 0) return 0;
@@ -1161,7 +1183,8 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   const int rs_mode = (!a.a_rowsum || !g8) ? 0 : (splits > 1 ? 2 : 1);
   float* rs_out = rs_mode == 2 ? rs_part : a.a_rowsum;
 
-  if (g8) { if (cbf) dispatch_g8<bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
+  if (g8 && bf) { if (cbf) dispatch_g8<bf16, bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
+  else if (g8) dispatch_g8<float, float>(a, e, ws, splits, tps, rs_out, rs_mode, s);
   else if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
   else { if (cbf) dispatch_layout<float, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<float, float>(a, e, ws, splits, tps, s); }
   MMFD_CHECK_LAUNCH("gemm_mfma");

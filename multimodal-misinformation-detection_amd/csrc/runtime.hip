@@ -41,6 +41,12 @@ __global__ void cast_f32_bf16_vec(const float4* __restrict__ in, uint4* __restri
   }
 }
 
+__global__ void zero_kernel(uint4* __restrict__ v, int64_t n16, unsigned char* __restrict__ tail, int64_t ntail) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) v[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntail; i += stride) tail[i] = 0;
+}
+
 template <typename T>
 __global__ void axpby_kernel(int64_t n, float a, const T* __restrict__ x, float b, const T* __restrict__ y,
                              T* __restrict__ out) {
@@ -100,6 +106,17 @@ extern "C" int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in,
     return mmfd_set_error(MMFD_ERR_INVALID, "mmfd_cast: bad dtypes %d->%d", dtype_in, dtype_out);
   }
   MMFD_CHECK_LAUNCH("cast");
+  return 0;
+}
+
+extern "C" int mmfd_zero(void* dst, int64_t bytes, mmfd_stream_t stream) {
+  if (bytes == 0) return 0;
+  MMFD_CHECK_ARG(dst != nullptr && bytes > 0, "mmfd_zero: bad buffer");
+  // a kernel, not hipMemsetAsync: identical inside captured HIP graphs and eager streams
+  const int64_t n16 = ((uintptr_t)dst & 15) == 0 ? bytes / 16 : 0;
+  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(std::max<int64_t>(n16, 1), 256)), dim3(256), 0, (hipStream_t)stream,
+                     (uint4*)dst, n16, (unsigned char*)dst + n16 * 16, bytes - n16 * 16);
+  MMFD_CHECK_LAUNCH("zero");
   return 0;
 }
 

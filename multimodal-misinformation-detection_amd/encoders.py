@@ -197,9 +197,9 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         dx = K.dropout(dx, st["emb_drop"]["dropout_p"], st["emb_drop"]["seed"], st["emb_drop"]["salt"])
     dsum, _ = Bk.layernorm_bwd(ctx, dx, st["s0"], "embeddings.LayerNorm", st["m0"], st["r0"])
     P = ctx.P
-    dword = torch.zeros_like(P["embeddings.word_embeddings.weight"])
-    dpos = torch.zeros_like(P["embeddings.position_embeddings.weight"])
-    dtyp = torch.zeros_like(P["embeddings.token_type_embeddings.weight"])
+    z = lambda n: K.zeros(P[n].shape, device=dsum.device)  # noqa: E731  (scatter-add targets)
+    dword, dpos, dtyp = (z("embeddings." + n) for n in ("word_embeddings.weight", "position_embeddings.weight",
+                                                          "token_type_embeddings.weight"))
     K.embed_bwd(ids, tts, dsum, dword, dpos, dtyp, padding_idx=cfg.pad_token_id)
     ctx.grads["embeddings.word_embeddings.weight"] = dword
     ctx.grads["embeddings.position_embeddings.weight"] = dpos
@@ -223,8 +223,7 @@ class _BertFn(torch.autograd.Function):
         ids = input_ids.to(dev).long().contiguous()
         B, L = ids.shape
         mask = attention_mask.to(dev).long().contiguous() if attention_mask is not None else None
-        tts = token_type_ids.to(dev).long().contiguous() if token_type_ids is not None else \
-            torch.zeros_like(ids)
+        tts = token_type_ids.to(dev).long().contiguous() if token_type_ids is not None else None  # None = type 0
         out, st = bert_forward(sc, cfg, ids, mask, tts, keep)
         fctx.keep = keep
         if keep:

@@ -431,11 +431,14 @@ class SentenceEncoder:
         return torch.cat(outs) if len(outs) > 1 else outs[0]
 
     def encode(self, sentences, batch_size=256, convert_to_tensor=True):
+        """SentenceTransformer.encode: a str gives [768], a list [N, 768] (fp32, host)"""
         if self.tokenizer is None:
             raise RuntimeError("SentenceEncoder.encode needs a tokenizer (pass tokenizer=...); use encode_ids")
-        enc = self.tokenizer(list(sentences), padding=True, truncation=True, max_length=self.max_seq_length,
-                             return_tensors="pt")
+        single = isinstance(sentences, str)
+        enc = self.tokenizer([sentences] if single else list(sentences), padding=True, truncation=True,
+                             max_length=self.max_seq_length, return_tensors="pt")
         emb = self.encode_ids(enc["input_ids"], enc["attention_mask"], batch_size).cpu()
+        emb = emb[0] if single else emb
         return emb if convert_to_tensor else emb.numpy()
 
 

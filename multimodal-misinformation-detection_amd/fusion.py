@@ -71,7 +71,7 @@ def _repr_modality_fwd(ctx, cfg, Xin, m, unimodal):
     return Y.view(B, L, E), dict(Xin=Xin, X=X, qkv=qkv, st1=st1, st2=st2, st3=st3, m=m)
 
 
-def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin):
+def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin, out=None):
     r = "representation."
     m = st["m"]
     E = cfg.E
@@ -97,7 +97,9 @@ def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin):
     Wp, _ = ctx.w_packed(names)
     Bk.linear_dx(ctx, dqkv2, Wp, out=dX, beta=1.0)  # dX += dQKV [WQ;WK;WV]
     ctx.lin_grads([r + f"{m}_proj"], dX, Bk.as2d(st["Xin"]))
-    return Bk.linear_dx(ctx, dX, r + f"{m}_proj").view(st["Xin"].shape) if need_dxin else None
+    if not need_dxin:
+        return None
+    return Bk.linear_dx(ctx, dX, r + f"{m}_proj", out=out).view(st["Xin"].shape)
 
 
 # -------------------------------------------------------------------------------------------------
@@ -135,7 +137,7 @@ def _cond_fwd(ctx, cfg, Hs, Es):
     return out, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
 
 
-def _cond_bwd(ctx, cfg, dS, cst, need_dE):
+def _cond_bwd(ctx, cfg, dS, cst, need_dE, out_dE=None):
     """dS: tag -> [B, L, E] grads. Returns (dH per claim modality (2-D), dE per evidence modality)."""
     c = "cross_attn."
     E = cfg.E
@@ -173,7 +175,7 @@ def _cond_bwd(ctx, cfg, dS, cst, need_dE):
         ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]))
         if need_dE.get(em):
             Wp, _ = ctx.w_packed(names)
-            dE[em] = Bk.linear_dx(ctx, dkv2, Wp).view(cst["Es"][em].shape)
+            dE[em] = Bk.linear_dx(ctx, dkv2, Wp, out=(out_dE or {}).get(em)).view(cst["Es"][em].shape)
     return dH, dE
 
 
@@ -251,8 +253,11 @@ def head_forward(ctx, cfg: HeadConfig, X_t, X_i, E_t, E_i):
     return outs, state
 
 
-def head_backward(ctx, cfg: HeadConfig, douts, state, need_dX=(True, True), need_dE=(True, True)):
-    """douts: dict tag -> fp32 grad of logits. Returns dX_t, dX_i, dE_t, dE_i (compute dtype or None)."""
+def head_backward(ctx, cfg: HeadConfig, douts, state, need_dX=(True, True), need_dE=(True, True), outs=None):
+    """douts: dict tag -> fp32 grad of logits. Returns dX_t, dX_i, dE_t, dE_i (compute dtype or None).
+    `outs` (optional 4-tuple of 2-D compute-dtype buffers or None) receive them in place: the halves
+    of the stacked claim/evidence encoder-output gradient (FusionTrainer, no split/concat copies)."""
+    outs = outs or (None, None, None, None)
     S = state["S"]
     hst = state["hst"]
     dS = {}
@@ -268,10 +273,10 @@ def head_backward(ctx, cfg: HeadConfig, douts, state, need_dX=(True, True), need
             dp = _mlp_head_bwd(ctx, douts[t], st)
             dS[t] = K.seq_mean_bwd(dp, S[t].shape[1])
     need_e = {"text": need_dE[0], "image": need_dE[1]}
-    dH, dE = _cond_bwd(ctx, cfg, dS, state["cst"], need_e)
+    dH, dE = _cond_bwd(ctx, cfg, dS, state["cst"], need_e, out_dE={"text": outs[2], "image": outs[3]})
     dX = {}
     for m, st in state["rst"].items():
         need = need_dX[0] if m == "text" else need_dX[1]
         if m in dH:
-            dX[m] = _repr_modality_bwd(ctx, cfg, dH[m], st, need)
+            dX[m] = _repr_modality_bwd(ctx, cfg, dH[m], st, need, out=outs[0] if m == "text" else outs[1])
     return dX.get("text"), dX.get("image"), dE.get("text"), dE.get("image")

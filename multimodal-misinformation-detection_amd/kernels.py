@@ -1,8 +1,16 @@
-"""ctypes binding of libmmfd_hip.so (the C ABI declared in include/mmfd.h) plus thin torch-tensor
+"""Host bindings of libmmfd_hip.so (the C ABI declared in include/mmfd.h) plus thin torch-tensor
 wrappers. PyTorch only provides device memory, the current HIP stream and autograd plumbing; every
 computation below is a launch of one of our gfx950 kernels.
 
-There is no fallback: if the shared library is missing or cannot be loaded, every op raises
+Two layers over the same C ABI:
+  * the training / retrieval hot path (GEMM, attention, LayerNorm, cross entropy, AdamW, sequence
+    mean, cast, cosine scores, top-k) goes through the PyTorch custom ops torch.ops.mmfd.* that
+    libmmfd_torch.so registers (csrc/torch_ops.cpp: TORCH_LIBRARY schemas with declared
+    mutations, CUDA/HIP dispatch; fake kernels in mmfd/ops.py);
+  * the remaining entry points (encoder embeddings, ResNet / Swinv2 / DeBERTa helpers,
+    preprocessing) are called through ctypes.
+
+There is no fallback: if either shared library is missing or cannot be loaded, every op raises
 `NativeLibraryError` (the product path must never silently run on something else).
 """
 from __future__ import annotations
@@ -15,10 +23,11 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMFD_LIB_PATH") or os.path.join(_HERE, "libmmfd_hip.so")  # env override: A/B runs of two builds (tools/ab.sh)
+TORCH_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libmmfd_torch.so")
 
 F32, BF16, F16 = 0, 1, 2
 COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4
-ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
 
 
 class NativeLibraryError(RuntimeError):
@@ -129,6 +138,7 @@ SIGNATURES = {
     "mmfd_vit_tokens_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     "mmfd_adamw": (_I, [_I, _VP, _I64, _F, _F, _F, _F, _F, _VP]),
     "mmfd_cast": (_I, [_I, _I, _I64, _VP, _VP, _VP]),
+    "mmfd_zero": (_I, [_VP, _I64, _VP]),
     "mmfd_axpby": (_I, [_I, _I64, _F, _VP, _F, _VP, _VP, _VP]),
     "mmfd_dropout": (_I, [_I, _I64, _VP, _VP, _F, _VP, _U64, _VP]),
     "mmfd_seed_advance": (_I, [_VP, _VP]),
@@ -163,8 +173,27 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not os.path.exists(TORCH_LIB_PATH):
+        raise NativeLibraryError(f"{TORCH_LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        torch.ops.load_library(TORCH_LIB_PATH)  # registers torch.ops.mmfd.* (needs libmmfd_hip.so loaded)
+    except (OSError, RuntimeError) as e:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load {TORCH_LIB_PATH}: {e}") from e
+    from . import ops  # noqa: F401  (fake kernels of the custom ops)
     _lib = lib
     return lib
+
+
+def _ops():
+    if _lib is None:
+        load()
+    return torch.ops.mmfd
+
+
+def _salt(salt):
+    """uint64 call-site salt -> the int64 of the op schema (same bits)"""
+    salt = int(salt) & 0xFFFFFFFFFFFFFFFF
+    return salt - (1 << 64) if salt >= (1 << 63) else salt
 
 
 def lib():
@@ -259,6 +288,7 @@ class GemmProbe:
         _PROBE = None
 
     def summary(self):
+        """per kernel instantiation {launches, flops, ms}"""
         torch.cuda.synchronize()
         out = {}
         for key, flops, e0, e1 in self.records:
@@ -273,10 +303,13 @@ class GemmProbe:
 def _kernel_name(a, split):
     """the device kernel mmfd_gemm launches for these arguments (rocprof's demangled name)"""
     t = {F32: "float", BF16: "__bf16"}
-    if a.dtype == BF16:  # 256x256 kernel (gemm.hip use_g8); PRE = one prefetched epilogue operand stream
+    narrow = a.M >= 4096 and (a.N <= 128 or a.K < 64)  # gemm.hip use_g8
+    g8 = not narrow and (a.dtype == BF16 or a.c_dtype == F32)
+    if g8:  # 256x256 kernel; PRE = one prefetched bf16 epilogue operand stream
         streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD)) + int(a.beta != 0.0)
         pre = a.c_dtype == BF16 and streams == 1 and not split
-        base = f"gemm256_kernel<{a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, {'true' if pre else 'false'}>"
+        base = (f"gemm256_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
+                f"{'true' if pre else 'false'}>")
     else:
         base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")
@@ -312,47 +345,41 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
             raise ValueError("residual/aux must match the output shape and dtype")
     if dropout_p > 0 and seed is None:
         raise ValueError("dropout needs a Seed")
-    a = GemmArgs()
-    a.dtype = dtype_code(A.dtype)
-    a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
-    a.M, a.N, a.K = M, N, K
-    a.A, a.lda = A.data_ptr(), _ld(A)
-    a.B, a.ldb = B.data_ptr(), _ld(B)
-    a.C, a.ldc, a.c_dtype = out.data_ptr(), _ld(out), dtype_code(out.dtype)
-    a.alpha, a.beta = float(alpha), float(beta)
-    a.ep.bias = bias.data_ptr() if bias is not None else None
-    if residual is not None:
-        a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
-        a.ep.residual_first = int(bool(residual_first))
-    if aux is not None:
-        a.ep.aux, a.ep.ldaux = aux.data_ptr(), _ld(aux)
-    a.ep.act = int(act)
-    a.ep.dropout_p = float(dropout_p)
-    a.ep.seed = seed.t.data_ptr() if seed is not None else None
-    a.ep.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
-    a.splits = int(splits)
     if a_rowsum is not None:
         if a_rowsum.dtype != torch.float32 or a_rowsum.numel() != M or not a_rowsum.is_contiguous():
             raise ValueError("a_rowsum must be a contiguous fp32 vector of length M")
         _require_cuda(a_rowsum)
-        a.a_rowsum, a.a_rowsum_beta = a_rowsum.data_ptr(), float(a_rowsum_beta)
-    L = lib()
-    need = L.mmfd_gemm_workspace_bytes(ctypes.byref(a))
-    ws = None
-    if need > 0:
-        ws = torch.empty(need // 4 + 1, device=A.device, dtype=torch.float32)
-        a.workspace, a.workspace_bytes = ws.data_ptr(), need
     probe = _PROBE
-    rec = probe is not None and M >= 16 and N >= 16 and K >= 16
+    rec = probe is not None and M >= 16 and N >= 16 and K >= 16 and not torch.cuda.is_current_stream_capturing()
     if rec:
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    _check(L.mmfd_gemm(ctypes.byref(a), _stream()), "mmfd_gemm")
+    _ops().gemm(A, B, bool(trans_a), bool(trans_b), out, float(alpha), float(beta), bias, residual,
+                bool(residual_first), int(act), aux, float(dropout_p), seed.t if seed is not None else None,
+                _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta))
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        probe.records.append((_kernel_name(a, need > 0), 2 * M * N * K, e0, e1))
+        probe.records.append((_probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits), 2 * M * N * K,
+                              e0, e1))
     return out
+
+
+def _probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits):
+    """the kernel instantiation mmfd_gemm picks (GemmProbe bookkeeping only)"""
+    M, K = (A.shape[1], A.shape[0]) if trans_a else A.shape
+    N = B.shape[1] if trans_b else B.shape[0]
+    a = GemmArgs()
+    a.dtype, a.c_dtype = dtype_code(A.dtype), dtype_code(out.dtype)
+    a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
+    a.M, a.N, a.K = M, N, K
+    a.A, a.lda, a.B, a.ldb = A.data_ptr(), _ld(A), B.data_ptr(), _ld(B)
+    a.C, a.ldc = out.data_ptr(), _ld(out)
+    a.beta, a.splits = float(beta), int(splits)
+    if residual is not None:
+        a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
+    a.ep.act = int(act)
+    return _kernel_name(a, lib().mmfd_gemm_workspace_bytes(ctypes.byref(a)) > 0)
 
 
 def colsum(X, out=None, beta=0.0):
@@ -396,26 +423,13 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
     if out is None:
         out = torch.empty((B, Lq, H * D), device=q.device, dtype=q.dtype)
     lse = torch.empty((B, H, Lq), device=q.device, dtype=torch.float32)
-    a = AttnArgs()
-    a.dtype = dtype_code(q.dtype)
-    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
-    a.scale = float(scale if scale is not None else D ** -0.5)
-    a.q, a.q_sb, a.q_st = _head_view(q, H, D)
-    a.k, a.k_sb, a.k_st = _head_view(k, H, D)
-    a.v, a.v_sb, a.v_st = _head_view(v, H, D)
-    a.o, a.o_sb, a.o_st = _head_view(out, H, D)
-    a.lse = lse.data_ptr()
-    a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias, a.rel_bias_sb, a.rel_bias_mod = _rel_bias_args(rel_bias, B, H, Lq, Lk)
-    a.dropout_p = float(dropout_p)
-    a.seed = seed.t.data_ptr() if seed is not None else None
-    a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
-    if cos_logit_scale is not None:
-        if cos_logit_scale.dtype != torch.float32 or not cos_logit_scale.is_contiguous():
-            raise ValueError("cos_logit_scale must be a contiguous fp32 tensor of H values")
-        a.cos_logit_scale = cos_logit_scale.data_ptr()
-        a.cos_max_log = float(cos_max_log)
-    _check(lib().mmfd_attn_fwd(ctypes.byref(a), _stream()), "mmfd_attn_fwd")
+    _head_view(q, H, D), _head_view(k, H, D), _head_view(v, H, D), _head_view(out, H, D)
+    rb, rb_sb, rb_mod = _rel_bias_args(rel_bias, B, H, Lq, Lk)
+    if cos_logit_scale is not None and (cos_logit_scale.dtype != torch.float32 or not cos_logit_scale.is_contiguous()):
+        raise ValueError("cos_logit_scale must be a contiguous fp32 tensor of H values")
+    _ops().attn_fwd(q, k, v, out, lse, int(H), float(scale if scale is not None else D ** -0.5), key_bias,
+                    rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
+                    seed.t if seed is not None else None, _salt(salt), cos_logit_scale, float(cos_max_log))
     return out, lse
 
 
@@ -478,28 +492,12 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
     dq = dq if dq is not None else torch.empty_like(q, memory_format=torch.contiguous_format)
     dk = dk if dk is not None else torch.empty((B, Lk, HD), device=q.device, dtype=q.dtype)
     dv = dv if dv is not None else torch.empty((B, Lk, HD), device=q.device, dtype=q.dtype)
-    delta = torch.empty((B, H, Lq), device=q.device, dtype=torch.float32)
-    a = AttnArgs()
-    a.dtype = dtype_code(q.dtype)
-    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
-    a.scale = float(scale if scale is not None else D ** -0.5)
-    a.q, a.q_sb, a.q_st = _head_view(q, H, D)
-    a.k, a.k_sb, a.k_st = _head_view(k, H, D)
-    a.v, a.v_sb, a.v_st = _head_view(v, H, D)
-    a.o, a.o_sb, a.o_st = _head_view(o, H, D)
-    a.lse = lse.data_ptr()
-    a.key_bias = key_bias.data_ptr() if key_bias is not None else None
-    a.rel_bias, a.rel_bias_sb, a.rel_bias_mod = _rel_bias_args(rel_bias, B, H, Lq, k.shape[1])
-    a.dropout_p = float(dropout_p)
-    a.seed = seed.t.data_ptr() if seed is not None else None
-    a.salt = int(salt) & 0xFFFFFFFFFFFFFFFF
-    a.dout, a.do_sb, a.do_st = _head_view(dout, H, D)
-    a.dq, a.dq_sb, a.dq_st = _head_view(dq, H, D)
-    a.dk, a.dk_sb, a.dk_st = _head_view(dk, H, D)
-    a.dv, a.dv_sb, a.dv_st = _head_view(dv, H, D)
-    a.delta = delta.data_ptr()
-    a.accumulate_dq, a.accumulate_dkv = int(accumulate_dq), int(accumulate_dkv)
-    _check(lib().mmfd_attn_bwd(ctypes.byref(a), _stream()), "mmfd_attn_bwd")
+    for t in (q, k, v, o, dout, dq, dk, dv):
+        _head_view(t, H, D)
+    rb, rb_sb, rb_mod = _rel_bias_args(rel_bias, B, H, Lq, Lk)
+    _ops().attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, int(H), float(scale if scale is not None else D ** -0.5),
+                    key_bias, rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
+                    seed.t if seed is not None else None, _salt(salt), bool(accumulate_dq), bool(accumulate_dkv))
     return dq, dk, dv
 
 
@@ -512,9 +510,7 @@ def layernorm_fwd(x2d, gamma, beta, eps, out=None):
     y = out if out is not None else torch.empty((R, W), device=x2d.device, dtype=x2d.dtype)
     mean = torch.empty(R, device=x2d.device, dtype=torch.float32)
     rstd = torch.empty(R, device=x2d.device, dtype=torch.float32)
-    _check(lib().mmfd_layernorm_fwd(dtype_code(x2d.dtype), R, W, _ptr(x2d), _ld(x2d), _ptr(gamma), _ptr(beta),
-                                    float(eps), _ptr(y), _ld(y), _ptr(mean), _ptr(rstd), _stream()),
-           "mmfd_layernorm_fwd")
+    _ops().layernorm_fwd(x2d, gamma, beta, float(eps), y, mean, rstd)
     return y, mean, rstd
 
 
@@ -539,14 +535,8 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None
     _require_cuda(dy, x, gamma, mean, rstd)
     R, W = dy.shape
     dx = dx if dx is not None else torch.empty((R, W), device=dy.device, dtype=dy.dtype)
-    nb = max(1, min((R + 3) // 4, 2048))
-    ws = torch.empty(nb * 2 * W, device=dy.device, dtype=torch.float32)
-    _check(lib().mmfd_layernorm_bwd(dtype_code(dy.dtype), R, W, _ptr(dy), _ld(dy), _ptr(x), _ld(x), _ptr(gamma),
-                                    _ptr(mean), _ptr(rstd), _ptr(dx), _ld(dx), _ptr(dx_add),
-                                    _ld(dx_add) if dx_add is not None else 0, _ptr(dgamma), _ptr(dbeta),
-                                    float(beta_acc), _ptr(dx_drop), float(dropout_p),
-                                    seed.ptr() if seed is not None else None, int(salt) & 0xFFFFFFFFFFFFFFFF,
-                                    _ptr(ws), ws.numel() * 4, _stream()), "mmfd_layernorm_bwd")
+    _ops().layernorm_bwd(dy, x, gamma, mean, rstd, dx, dx_add, dgamma, dbeta, float(beta_acc), dx_drop,
+                         float(dropout_p), seed.t if seed is not None else None, _salt(salt))
     return dx
 
 
@@ -556,16 +546,14 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None
 def seq_mean_fwd(x, out=None):
     B, L, D = x.shape
     out = out if out is not None else torch.empty((B, D), device=x.device, dtype=x.dtype)
-    _check(lib().mmfd_seq_mean_fwd(dtype_code(x.dtype), B, L, D, _ptr(x.contiguous()), _ptr(out), _ld(out),
-                                   _stream()), "mmfd_seq_mean_fwd")
+    _ops().seq_mean_fwd(x if x.is_contiguous() else x.contiguous(), out)
     return out
 
 
 def seq_mean_bwd(dout, L, dx=None):
     B, D = dout.shape
     dx = dx if dx is not None else torch.empty((B, L, D), device=dout.device, dtype=dout.dtype)
-    _check(lib().mmfd_seq_mean_bwd(dtype_code(dout.dtype), B, L, D, _ptr(dout), _ld(dout), _ptr(dx), _stream()),
-           "mmfd_seq_mean_bwd")
+    _ops().seq_mean_bwd(dout, dx)
     return dx
 
 
@@ -586,13 +574,10 @@ def xent_fwd_bwd(logits, labels, want_grad=True, dloss_scale=None, cols=None, n_
     ld = labels.stride(0) if labels.dim() > 1 else 1
     if max(cols) >= (labels.shape[1] if labels.dim() > 1 else 1):
         raise ValueError(f"xent: label column {max(cols)} outside labels {tuple(labels.shape)}")
+    del ld
     loss = torch.empty(n_slots, device=dev, dtype=torch.float32)
-    lp = (ctypes.c_void_p * n)(*[l.data_ptr() for l in logits])
-    cp = (ctypes.c_int * n)(*cols)
     dl = [torch.empty_like(l) for l in logits] if want_grad else None
-    dp = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dl]) if want_grad else None
-    _check(lib().mmfd_xent_fwd_bwd(n, B, C, lp, cp, _ptr(labels), ld, _ptr(loss), int(n_slots), dp,
-                                   _ptr(dloss_scale), _stream()), "mmfd_xent_fwd_bwd")
+    _ops().xent(logits, cols, labels, loss, dl if want_grad else [], dloss_scale)
     return loss, dl
 
 
@@ -602,9 +587,22 @@ def cast(x, dtype, out=None):
     elif out.dtype != dtype or out.numel() != x.numel() or not out.is_contiguous():
         raise ValueError("cast: out must be a contiguous tensor of the target dtype and size")
     if x.numel():
-        _check(lib().mmfd_cast(dtype_code(x.dtype), dtype_code(dtype), x.numel(), _ptr(x.contiguous()), _ptr(out),
-                               _stream()), "mmfd_cast")
+        _ops().cast(x if x.is_contiguous() else x.contiguous(), out)
     return out
+
+
+def zero_(t):
+    """t[...] = 0 in place (a contiguous tensor) with mmfd_zero (a zero-fill kernel on the current stream)"""
+    if not t.is_contiguous():
+        raise ValueError("zero_: contiguous tensors only")
+    if t.numel():
+        _check(lib().mmfd_zero(_ptr(t), t.numel() * t.element_size(), _stream()), "mmfd_zero")
+    return t
+
+
+def zeros(shape, dtype=torch.float32, device="cuda"):
+    """torch.empty + mmfd_zero"""
+    return zero_(torch.empty(shape, dtype=dtype, device=device))
 
 
 def axpby(a, x, b=0.0, y=None, out=None):
@@ -771,8 +769,8 @@ def vit_tokens_bwd(dout, want_dpatch=True):
 
 
 def adamw(table_dev, n, max_numel, lr, beta1, beta2, eps, weight_decay):
-    _check(lib().mmfd_adamw(int(n), _ptr(table_dev), int(max_numel), float(lr), float(beta1), float(beta2),
-                            float(eps), float(weight_decay), _stream()), "mmfd_adamw")
+    _ops().adamw(table_dev, int(n), int(max_numel), float(lr), float(beta1), float(beta2), float(eps),
+                 float(weight_decay))
 
 
 def dropout_hash(seed: int, salt: int, index: int) -> int:
@@ -800,8 +798,8 @@ def cosine_scores(queries, corpus, mode=COS_PAIR, eps=1e-6, out=None):
         raise TypeError(f"unsupported corpus dtype {corpus.dtype}")
     if out is None:
         out = torch.empty(Q, N, device=corpus.device, dtype=torch.float32)
-    _check(lib().mmfd_cosine_scores(_CORPUS_CODES[corpus.dtype], Q, N, D, _ptr(queries), D, _ptr(corpus), _ld(corpus),
-                                    int(mode), float(eps), _ptr(out), _ld(out), _stream()), "mmfd_cosine_scores")
+    _ld(corpus)
+    _ops().cosine_scores(queries, corpus, int(mode), float(eps), out)
     return out
 
 
@@ -812,10 +810,8 @@ def topk(scores, k):
     Q, N = scores.shape
     val = torch.empty(Q, k, device=scores.device, dtype=torch.float32)
     idx = torch.empty(Q, k, device=scores.device, dtype=torch.int64)
-    nbytes = lib().mmfd_topk_workspace_bytes(Q, N, k)
-    ws = torch.empty(max(nbytes, 8), device=scores.device, dtype=torch.uint8)
-    _check(lib().mmfd_topk(Q, N, _ptr(scores), _ld(scores), k, _ptr(val), _ptr(idx), _ptr(ws), nbytes, _stream()),
-           "mmfd_topk")
+    _ld(scores)
+    _ops().topk(scores, int(k), val, idx)
     return val, idx
 
 

@@ -12,14 +12,31 @@ import torch.nn as nn
 
 from . import kernels as K
 
-_SEED = {}
+_COUNT = {"mlp": 0, "mha": 0}
 
 
-def _seed_for(device):
-    s = _SEED.get(device)
-    if s is None:
-        s = _SEED[device] = K.Seed(0, device=device)
-    return s.fork()
+def _next_name(kind):
+    """default dropout site of a standalone layer: its kind and construction index ("mlp0",
+    "mha1", ...), identical from run to run (a Python object id is not)"""
+    n = _COUNT[kind]
+    _COUNT[kind] += 1
+    return f"{kind}{n}"
+
+
+class _Seeded:
+    """device-resident dropout seed of a standalone layer (manual_seed; advanced by every training
+    forward, as the fused model's seeds are)"""
+
+    def manual_seed(self, seed: int):
+        self._seed_value = int(seed)
+        if getattr(self, "_seed", None) is not None:
+            self._seed.set(self._seed_value)
+        return self
+
+    def _fork_seed(self, device):
+        if getattr(self, "_seed", None) is None or self._seed.t.device != device:
+            self._seed = K.Seed(getattr(self, "_seed_value", 0), device=device)
+        return self._seed.fork()
 
 
 class _LinearFn(torch.autograd.Function):
@@ -53,9 +70,8 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
-def linear(x, layer: nn.Linear, act=False, p=0.0, site=""):
-    seed = _seed_for(x.device) if p > 0 else None
-    return _LinearFn.apply(x, layer.weight, layer.bias, act, p, seed, site)
+def linear(x, layer: nn.Linear, act=False, p=0.0, site="", seed=None):
+    return _LinearFn.apply(x, layer.weight, layer.bias, act, p, seed if p > 0 else None, site)
 
 
 class _AttnFn(torch.autograd.Function):
@@ -76,38 +92,43 @@ class _AttnFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None
 
 
-class MLP(nn.Module):
-    """layers.py:5-21: Linear -> GELU -> Dropout -> Linear -> Dropout"""
+class MLP(_Seeded, nn.Module):
+    """layers.py:5-21: Linear -> GELU -> Dropout -> Linear -> Dropout. Dropout masks come from the
+    counter hash keyed by (seed, site): sites "<name>.h" / "<name>.out" (oracle.fusion_head.mlp)."""
 
-    def __init__(self, embed_dim, mlp_ratio=4.0, dropout=0.1):
+    def __init__(self, embed_dim, mlp_ratio=4.0, dropout=0.1, name=None):
         super().__init__()
         hidden_dim = int(embed_dim * mlp_ratio)
         self.net = nn.Sequential(nn.Linear(embed_dim, hidden_dim), nn.GELU(), nn.Dropout(dropout),
                                  nn.Linear(hidden_dim, embed_dim), nn.Dropout(dropout))
         self.dropout = dropout
+        self.site = name or _next_name("mlp")
 
     def forward(self, x):
         p = self.dropout if self.training else 0.0
-        h = linear(x, self.net[0], act=True, p=p, site=f"mlp{id(self)}.h")
-        return linear(h, self.net[3], p=p, site=f"mlp{id(self)}.out")
+        seed = self._fork_seed(x.device) if p > 0 else None
+        h = linear(x, self.net[0], act=True, p=p, site=self.site + ".h", seed=seed)
+        return linear(h, self.net[3], p=p, site=self.site + ".out", seed=seed)
 
 
-class MultiHeadAttention(nn.Module):
+class MultiHeadAttention(_Seeded, nn.Module):
     """layers.py:24-58: softmax(Q K^T / sqrt(hd)) (no mask), attention dropout, out_proj. The eager
-    and `fused_attn` (SDPA) branches are the same computation here (one flash-style kernel)."""
+    and `fused_attn` (SDPA) branches are the same computation here (one flash-style kernel).
+    Attention-probability dropout site: "<name>.attn" (oracle.fusion_head.mha)."""
 
-    def __init__(self, embed_dim, num_heads, dropout=0.1, fused_attn=False):
+    def __init__(self, embed_dim, num_heads, dropout=0.1, fused_attn=False, name=None):
         super().__init__()
         self.embed_dim = embed_dim
         self.num_heads = num_heads
         self.dropout = dropout
         self.fused_attn = fused_attn
         self.attn_dropout = nn.Dropout(dropout)
+        self.site = name or _next_name("mha")
 
     def forward(self, Q, K_, V, out_proj):
         p = self.dropout if self.training else 0.0
-        seed = _seed_for(Q.device) if p > 0 else None
-        ctx = _AttnFn.apply(Q, K_, V, self.num_heads, p, seed, f"mha{id(self)}")
+        seed = self._fork_seed(Q.device) if p > 0 else None
+        ctx = _AttnFn.apply(Q, K_, V, self.num_heads, p, seed, self.site + ".attn")
         if isinstance(out_proj, nn.Linear):
             return linear(ctx, out_proj)
         return out_proj(ctx)

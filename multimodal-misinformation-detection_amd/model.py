@@ -107,15 +107,24 @@ class ClassificationModule(nn.Module):
 
 class _HeadFn(torch.autograd.Function):
     """The whole fusion head as one autograd node (forward: fusion.head_forward, backward:
-    fusion.head_backward). Outputs: (y_tt, y_ti, y_it, y_ii) or (pred,) — None for absent paths."""
+    fusion.head_backward). Outputs: (y_tt, y_ti, y_it, y_ii) or (pred,) — None for absent paths.
+    With `pairs_B` > 0 the text / image inputs are the STACKED encoder outputs [2B, L, D] of
+    FusionTrainer (claims rows [:B], evidence rows [B:]): the backward then writes dX and dE into
+    the two halves of one gradient buffer per modality instead of two slice-backward scatters."""
 
     @staticmethod
-    def forward(ctx, model, X_t, X_i, E_t, E_i, *params):
+    def forward(ctx, model, pairs_B, X_t, X_i, E_t, E_i, *params):
         names = model._param_names
         P = {n: p.detach() for n, p in zip(names, params)}
         sc = Bk.StepCtx(P, model.compute_dtype, model.dropout_p, model._get_seed() if model.training else None,
                         training=model.training, shadows=Bk.shadow_store(model))
         sc.grad_ready = getattr(model, "_grad_ready", None)
+        ctx.pairs_B = pairs_B
+        ctx.stacked = [None if x is None else (x.shape, x.dtype) for x in (X_t, X_i)] if pairs_B else None
+        if pairs_B:
+            (T, I), B = (X_t, X_i), pairs_B
+            X_t, E_t = (T[:B], T[B:]) if T is not None else (None, None)
+            X_i, E_i = (I[:B], I[B:]) if I is not None else (None, None)
         outs, state = FU.head_forward(sc, model._cfg, X_t, X_i, E_t, E_i)
         ctx.sc, ctx.state, ctx.model = sc, state, model
         ctx.in_shapes = [None if x is None else (x.shape, x.dtype) for x in (X_t, X_i, E_t, E_i)]
@@ -137,8 +146,35 @@ class _HeadFn(torch.autograd.Function):
             douts[t] = g.contiguous().float() if g is not None else torch.zeros(shp, device=state["S"][
                 next(iter(state["S"]))].device, dtype=torch.float32)
         need = ctx.needs_input_grad
-        dXt, dXi, dEt, dEi = FU.head_backward(sc, model._cfg, douts, state, need_dX=(need[1], need[2]),
-                                              need_dE=(need[3], need[4]))
+        if ctx.pairs_B:
+            B = ctx.pairs_B
+            bufs, outs = [], []
+            for i, st in enumerate(ctx.stacked):
+                if st is None or not need[2 + i]:
+                    bufs.append(None)
+                    outs += [None, None]
+                    continue
+                buf = torch.empty(st[0], device=douts[ctx.tags[0]].device, dtype=st[1])
+                bufs.append(buf)
+                direct = st[1] == sc.dt  # the GEMMs write the halves directly
+                outs += [Bk.as2d(buf[:B]) if direct else None, Bk.as2d(buf[B:]) if direct else None]
+            nt, ni = bufs[0] is not None, bufs[1] is not None
+            dXt, dXi, dEt, dEi = FU.head_backward(sc, model._cfg, douts, state, need_dX=(nt, ni), need_dE=(nt, ni),
+                                                  outs=(outs[0], outs[2], outs[1], outs[3]))
+            sc.flush_ready()
+            for buf, (a, b), (oa, ob) in zip(bufs, ((dXt, dEt), (dXi, dEi)), ((outs[0], outs[1]), (outs[2], outs[3]))):
+                if buf is None:
+                    continue
+                for d, o, half in ((a, oa, buf[:B]), (b, ob, buf[B:])):
+                    if d is None:  # no path consumed these rows (text_only / unimodal heads)
+                        K.zero_(half)
+                    elif o is None:  # compute dtype differs from the encoders' output dtype
+                        K.cast(d.contiguous(), buf.dtype, out=half)
+            pgrads = [sc.grads.get(n) for n in model._param_names]
+            ctx.sc = ctx.state = None
+            return (None, None, bufs[0], bufs[1], None, None, *pgrads)
+        dXt, dXi, dEt, dEi = FU.head_backward(sc, model._cfg, douts, state, need_dX=(need[2], need[3]),
+                                              need_dE=(need[4], need[5]))
         sc.flush_ready()
 
         def back(d, shp):
@@ -146,11 +182,11 @@ class _HeadFn(torch.autograd.Function):
                 return None
             return d if d.dtype == shp[1] else K.cast(d, shp[1])
 
-        dxs = [back(d, s) if need[i + 1] else None for i, (d, s) in enumerate(zip((dXt, dXi, dEt, dEi),
+        dxs = [back(d, s) if need[i + 2] else None for i, (d, s) in enumerate(zip((dXt, dXi, dEt, dEi),
                                                                                    ctx.in_shapes))]
         pgrads = [sc.grads.get(n) for n in model._param_names]
         ctx.sc = ctx.state = None
-        return (None, *dxs, *pgrads)
+        return (None, None, *dxs, *pgrads)
 
 
 class MisinformationDetectionModel(Bk.CachedWeights, nn.Module):
@@ -213,7 +249,18 @@ class MisinformationDetectionModel(Bk.CachedWeights, nn.Module):
         params = [p for _, p in self.named_parameters()]
         if not params[0].is_cuda:
             raise RuntimeError("mmfd MisinformationDetectionModel runs on the HIP device: call .to('cuda') first")
-        outs = _HeadFn.apply(self, X_t, X_i, E_t, E_i, *params)
+        outs = _HeadFn.apply(self, 0, X_t, X_i, E_t, E_i, *params)
+        if self.factify or self.text_only:
+            return outs[0], None
+        return (outs[0], outs[1]), (outs[2], outs[3])
+
+    def forward_pairs(self, T, I, B):
+        """forward(T[:B], I[:B], T[B:], I[B:]) on stacked claim/evidence encoder outputs (T / I
+        [2B, L, D]); their gradients come back as one tensor each (FusionTrainer)."""
+        params = [p for _, p in self.named_parameters()]
+        if not params[0].is_cuda:
+            raise RuntimeError("mmfd MisinformationDetectionModel runs on the HIP device: call .to('cuda') first")
+        outs = _HeadFn.apply(self, int(B), T, I, None, None, *params)
         if self.factify or self.text_only:
             return outs[0], None
         return (outs[0], outs[1]), (outs[2], outs[3])

@@ -65,6 +65,34 @@ class AdamW(torch.optim.Optimizer):
             self._tables[key] = t
         return t
 
+    # ---- HIP-graph capture: the pointer table is late-bound ------------------------------------------
+    # Under stream capture the gradients are fresh graph-pool tensors whose table cannot be uploaded
+    # from the host (no synchronous copies while capturing). The captured launch reads a device table
+    # reserved here; finalize_capture() fills it once the captured step has assigned every .grad
+    # (the same tensors every replay writes).
+    def _capture_table(self, entries):
+        n = len(entries) * ctypes.sizeof(K.AdamWTensor)
+        t = torch.empty(n, dtype=torch.uint8, device=entries[0][0].device)
+        self._pending_capture = getattr(self, "_pending_capture", []) + [(t, entries)]
+        return t
+
+    @torch.no_grad()
+    def finalize_capture(self):
+        from .blocks import SHADOW_OF
+        for t, entries in getattr(self, "_pending_capture", []):
+            arr = (K.AdamWTensor * len(entries))()
+            for i, (p, g, m, v, st) in enumerate(entries):
+                sh = SHADOW_OF.get(p.data_ptr())
+                ok = sh is not None and sh[0].dtype == torch.bfloat16 and sh[0].numel() == p.numel()
+                arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
+                arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
+                arr[i].param_bf16 = sh[0].data_ptr() if ok else None
+                arr[i].step, arr[i].numel = st.data_ptr(), p.numel()
+            t.copy_(torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8))
+        # the captured launches read these tables at every replay: keep them alive with the graph
+        self._captured_tables = getattr(self, "_captured_tables", []) + [t for t, _ in self._pending_capture]
+        self._pending_capture = []
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -91,7 +119,10 @@ class AdamW(torch.optim.Optimizer):
             if not entries:
                 continue
             b1, b2 = group["betas"]
-            table = self._table(entries, entries[0][0].device)
+            if torch.cuda.is_current_stream_capturing():
+                table = self._capture_table(entries)
+            else:
+                table = self._table(entries, entries[0][0].device)
             K.adamw(table, len(entries), max(e[0].numel() for e in entries), group["lr"], b1, b2, group["eps"],
                     group["weight_decay"])
         return loss

@@ -15,8 +15,8 @@ pass computing the scores of a query batch (`mmfd_cosine_scores`) and an exact t
 (`mmfd_topk`). Only the final, already sorted candidate list comes back to the host, where the
 distinct-score filter walks it (it needs at most a few more candidates than `top_k`; the
 candidate count grows until the filter is satisfied or the corpus is exhausted).
-The MiniLM cross-encoder re-ranking of text2text_retrieval.py:68-118 is a separate model and is
-out of scope; `dedupe_by_score` is the shared distinct-score filter.
+The MiniLM cross-encoder re-ranking of text2text_retrieval.py:68-118 and the SemanticSimilarity
+class are in mmfd.rerank; `dedupe_by_score` is the shared distinct-score filter.
 """
 from __future__ import annotations
 

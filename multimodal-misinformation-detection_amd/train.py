@@ -127,19 +127,68 @@ class FusionTrainer:
             return category_loss(outs[0], labels)
         return path_losses(outs, labels)
 
+    def _head_forward(self, batch):
+        """the head on the batch's features; encoder outputs go in stacked (forward_pairs), so their
+        gradients come back as one tensor per encoder"""
+        if "claim_text_embeds" in batch or self.text_encoder is None or self.image_encoder is None:
+            return self.head(*self.features(batch))
+        dev = self._device()
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
+            T = self.text_encoder(input_ids=batch["input_ids"].to(dev, non_blocking=True),
+                                  attention_mask=batch["attention_mask"].to(dev, non_blocking=True)).last_hidden_state
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_image):
+            I = self.image_encoder(batch["pixel_values"].to(dev, non_blocking=True)).last_hidden_state
+        return self.head.forward_pairs(T, I, batch["labels"].shape[0])
+
     def step(self, batch, return_outputs=False):
         """one optimizer step; returns the device loss vector [total, tt, ti, it, ii] (and the
         logits with return_outputs)"""
         self.optimizer.zero_grad(set_to_none=True)
-        outs = self.head(*self.features(batch))
+        outs = self._head_forward(batch)
         loss = self.loss(outs, batch["labels"].to(self._device(), non_blocking=True))
         if self.dp is not None:
             self.dp.begin()
-        loss[0].backward()
+        # d total / d loss = [1, 0, 0, 0, 0]: one resident vector, no per-step fill kernels
+        g = getattr(self, "_dtotal", None)
+        if g is None or g.device != loss.device:
+            g = self._dtotal = torch.tensor([1.0] + [0.0] * (loss.numel() - 1), device=loss.device)
+        torch.autograd.backward(loss, g)
         if self.dp is not None:
             self.dp.finish()
         self.optimizer.step()
         return (loss, outs) if return_outputs else loss
+
+    # ---- the whole step as one HIP graph ------------------------------------------------------------
+    def capture(self, batch, warmup=2):
+        """Capture one full training step (encoders + head forward, backward, AdamW) on `batch` into
+        a HIP graph: replay() then runs it with one launch and no per-kernel host work (the dropout
+        seeds advance on the device, AdamW's pointer table is bound after capture). `batch` tensors
+        are the graph's static inputs: refill them in place (or pass a batch to replay) between
+        replays. Single process only (the DP all-reduce stays eager)."""
+        if self.dp is not None:
+            raise RuntimeError("capture(): the data-parallel step runs eagerly")
+        self._static = batch
+        s = torch.cuda.Stream(device=self._device())
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):  # optimizer state, weight shadows, kernel attributes
+                self.step(batch)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_loss = self.step(batch)
+        self.optimizer.finalize_capture()
+        self._graph = g
+        return self
+
+    def replay(self, batch=None):
+        """one captured training step; returns the (static) device loss vector"""
+        if batch is not None and batch is not self._static:
+            for k, v in self._static.items():
+                if torch.is_tensor(v):
+                    v.copy_(batch[k], non_blocking=True)
+        self._graph.replay()
+        return self._graph_loss
 
     @torch.no_grad()
     def predict(self, batch):
@@ -153,7 +202,7 @@ class FusionTrainer:
         try:
             if "labels" not in batch and "claim_text_embeds" not in batch:
                 batch = dict(batch, labels=torch.empty(batch["pixel_values"].shape[0] // 2))
-            return self.head(*self.features(batch))
+            return self._head_forward(batch)
         finally:
             for m, w in zip(mods, was):
                 m.train(w)

@@ -141,3 +141,18 @@ def mpnet_forward(P, input_ids, attention_mask=None, *, num_layers, num_heads, e
         x = F.layer_norm(_lin(P, p + ".output.dense", f) + x, (D,), P[p + ".output.LayerNorm.weight"],
                          P[p + ".output.LayerNorm.bias"], eps)
     return x
+
+
+def cross_encoder_forward(P, input_ids, attention_mask, token_type_ids, *, num_layers, num_heads, eps=1e-12,
+                          activation="sigmoid"):
+    """sentence-transformers 3.3.1 CrossEncoder.predict over HF BertForSequenceClassification
+    (num_labels 1), as text2text_retrieval.py:24, 69-79 call it: BERT (keys prefixed "bert."),
+    BertPooler tanh(dense(h[:, 0])), classifier Linear -> logits; CrossEncoder's default activation
+    for one label is Sigmoid (sentence-transformers is not installed here: its published behaviour
+    is restated; `activation=None` returns the raw logits)."""
+    B = {k[len("bert."):]: v for k, v in P.items() if k.startswith("bert.")}
+    h = bert_forward(B, input_ids, attention_mask, token_type_ids, num_layers=num_layers, num_heads=num_heads,
+                     eps=eps)
+    pooled = torch.tanh(_lin(P, "bert.pooler.dense", h[:, 0]))
+    logits = _lin(P, "classifier", pooled)
+    return torch.sigmoid(logits) if activation == "sigmoid" else logits

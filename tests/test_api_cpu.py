@@ -215,3 +215,24 @@ def test_misinformation_dataset_reads_npz_store(tmp_path):
     assert next(iter(get_dataloader(str(tmp_path / "train.csv"), batch_size=3, num_workers=0, pre_embed=True)))["labels"].shape == (3, 4)
     with pytest.raises(FileNotFoundError):
         MisinformationDataset(str(tmp_path / "missing.csv"), pre_embed=True)
+
+
+def test_custom_op_boundary_schemas_and_fake_kernels():
+    """torch.ops.mmfd.* (libmmfd_torch.so over the C ABI): schemas declare their mutated outputs,
+    and the fake kernels let the ops trace without a device (FakeTensorMode)."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    K.load()
+    ops = torch.ops.mmfd
+    for name in ("gemm", "linear", "attn_fwd", "attn_bwd", "layernorm_fwd", "layernorm_bwd", "xent", "adamw",
+                 "seq_mean_fwd", "seq_mean_bwd", "cast", "cosine_scores", "topk"):
+        assert hasattr(ops, name), name
+    sch = str(ops.gemm.default._schema)
+    assert "Tensor(a!) out" in sch and "Tensor(b!)? aux" in sch and "Tensor(c!)? a_rowsum" in sch
+    assert "Tensor(a!) out, Tensor(b!) lse" in str(ops.attn_fwd.default._schema)
+    with FakeTensorMode():
+        x = torch.empty(2, 5, 48, device="cuda")
+        w = torch.empty(24, 48, device="cuda")
+        assert ops.linear(x, w, None, 1).shape == (2, 5, 24)
+        out = torch.empty(10, 24, device="cuda")
+        ops.gemm(x.reshape(10, 48), w, False, False, out, 1.0, 0.0, None, None, False, 0, None, 0.0, None, 0, 0,
+                 None, 0.0)

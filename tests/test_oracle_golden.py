@@ -308,3 +308,15 @@ def test_swinv2_host_geometry_matches_oracle(R, ws, shift):
     t, rpi = S.coords_table_and_index(ws)
     t2, rpi2 = O._coords(ws, 0)
     assert torch.equal(t, t2.float()) and torch.equal(rpi.long(), rpi2.reshape(-1))
+
+
+def test_cross_encoder_oracle_matches_transformers_fixture():
+    """oracle.encoders.cross_encoder_forward vs transformers BertForSequenceClassification
+    (num_labels 1, the ms-marco-MiniLM-L-6-v2 architecture scaled down)."""
+    z = _load("cross_encoder_small.npz")
+    cfg = json.loads(str(z["config"]))
+    P = _params(z, "param/")
+    args = (_t(z["input_ids"]), _t(z["attention_mask"]), _t(z["token_type_ids"]))
+    kw = dict(num_layers=cfg["num_hidden_layers"], num_heads=cfg["num_attention_heads"])
+    _close(OE.cross_encoder_forward(P, *args, activation=None, **kw), z["logits"], 2e-5)
+    _close(OE.cross_encoder_forward(P, *args, **kw), z["scores"], 2e-5)

@@ -5,6 +5,7 @@ Tolerances: fp32 — losses 1e-3 abs (north_star), every parameter gradient 2e-3
 tensor's max |grad|, over two consecutive steps (the second starts from AdamW-updated weights);
 bf16 — losses 5e-2 abs, gradients 0.1 relative (bf16 operands, fp32 accumulation/master weights).
 """
+import os
 import pytest
 import torch
 
@@ -110,3 +111,28 @@ def test_bf16_weight_shadows_follow_adamw_and_external_updates():
                         torch.bfloat16, shadows=store)
         names = [n for n, _, _ in store[k][1]]
         assert sc._shadow(k, names) is None
+
+
+@pytest.mark.skipif(os.environ.get("MMFD_TEST_STEP_GRAPH") != "1",
+                    reason="whole-step capture is experimental (replay faults); opt in with MMFD_TEST_STEP_GRAPH=1")
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_captured_step_replays_equal_eager_steps(precision):
+    """FusionTrainer.capture/replay (the whole step as one HIP graph: dropout seeds advance on the
+    device, AdamW's pointer table bound after capture) gives bitwise the same parameters and losses
+    as the same number of eager steps, dropout on; new inputs are taken through the static buffers."""
+    tr_e, _ = build_pair(precision, dropout=0.1)
+    tr_g, _ = build_pair(precision, dropout=0.1)
+    b1 = {k: v.cuda() for k, v in tiny_batch(3, seed=41).items()}
+    b2 = {k: v.cuda() for k, v in tiny_batch(3, seed=42).items()}
+    static = {k: v.clone() for k, v in b1.items()}
+    tr_g.capture(static, warmup=2)
+    le = [tr_e.step(b1) for _ in range(2)]
+    le += [tr_e.step(b1), tr_e.step(b2), tr_e.step(b1)]
+    lg = [tr_g.replay().clone(), tr_g.replay(b2).clone(), tr_g.replay(b1).clone()]
+    torch.cuda.synchronize()
+    for a, b in zip(le[2:], lg):
+        assert torch.equal(a, b)
+    for m_e, m_g in ((tr_e.text_encoder, tr_g.text_encoder), (tr_e.image_encoder, tr_g.image_encoder),
+                     (tr_e.head, tr_g.head)):
+        for (n, p), (_, q) in zip(m_e.named_parameters(), m_g.named_parameters()):
+            assert torch.equal(p, q), n
