@@ -60,8 +60,7 @@ struct AT {
 template <typename T, int D>
 __device__ __forceinline__ int row_off(int r, int c) {
   constexpr int NCH = AT<T, D>::NCH;
-  constexpr int m = NCH >= 8 ? 7 : NCH - 1;
-  return r * AT<T, D>::RB + ((c ^ (r & m)) << 4);
+  return r * AT<T, D>::RB + ((c ^ (r & (NCH - 1))) << 4);
 }
 // TR image: 16-B chunk c of row r (layout chosen for the transposed operand reads)
 template <typename T, int D>
@@ -72,7 +71,9 @@ __device__ __forceinline__ int tr_chunk(int r, int c) {
     if (D == 64) return c ^ (r & 7);
     return c ^ (2 * ((r >> 2) & 1));
   }
-  return c ^ (4 * ((r >> 2) & 1));
+  // fp32: the ROW swizzle c ^ (r & (NCH-1)) again; the 4-byte transposed reads of rows r+4g
+  // (g = 0..3) then land in distinct 4-chunk groups at D = 64 (16 chunks per row)
+  return c ^ (r & (AT<T, D>::NCH - 1));
 }
 
 // stage 64 rows [row0, row0+64) of a (token-strided) head slice into an image
@@ -491,16 +492,23 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
 }
 
 // =================================================================================================
-// v2 kernels (bf16, Lq and Lk <= 256): one workgroup of 8 waves per (b, h). The whole K/V (forward,
-// dQ) or Q/dO (dK/dV) of the head is staged in LDS ONCE and every wave sweeps 16-row blocks against
-// it: no per-block restaging, no repeated K/V reads from L2, and the forward softmax is single pass
-// (all 16 S^T subtiles stay in registers, so no online rescaling).
+// v2 kernels (Lq and Lk <= 256; bf16 forward up to 512 keys): one workgroup of 8 waves per (b, h).
+// The whole K/V (forward, dQ) or Q/dO (dK/dV) of the head is staged in LDS ONCE and every wave
+// sweeps 16-row blocks against it: no per-block restaging and no repeated K/V reads from L2. Rows
+// are padded only to one MFMA k-chunk (bf16: 32, fp32: 16), so L = 197 computes on 224 / 208 rows
+// instead of the streaming kernels' 256.
 // =================================================================================================
-constexpr int V2_LMAX = 256;      // backward kernels (Q/dO or K/V images of the head)
-constexpr int V2_LMAX_FWD = 512;  // forward: K/V images of 512 keys (128 KB at D = 64) still fit the 160-KB LDS
-constexpr int V2_THREADS = 512;       // forward / dQ: 8 waves sharing one K/V image
-constexpr int V2_DKDV_THREADS = 256;
-template <int D> struct V2 { static constexpr bool DUAL = (D == 64); };  // row image == transposed image
+constexpr int V2_LMAX = 256;      // backward kernels (Q/dO or K/V images of the head); fp32 forward
+constexpr int V2_LMAX_FWD = 512;  // bf16 forward: K/V images of 512 keys (128 KB at D = 64) fit the 160-KB LDS
+constexpr int V2_THREADS = 512;   // forward / dQ: 8 waves sharing one K/V image
+// dK/dV: bf16 images are small enough for two workgroups per CU; an fp32 head image (up to 128 KB)
+// allows one, so it gets 8 waves
+template <typename T> struct V2T { static constexpr int DKDV_THREADS = sizeof(T) == 4 ? 512 : 256; };
+// row image == transposed image (no second copy): bf16 at D = 64 and every fp32 layout
+template <typename T, int D> struct V2 { static constexpr bool DUAL = sizeof(T) == 4 || D == 64; };
+// rows per MFMA k-chunk, and 16-row subtiles per chunk
+template <typename T> __host__ __device__ constexpr int v2_kc() { return sizeof(T) == 2 ? 32 : 16; }
+__host__ __device__ inline int v2_pad(int64_t n, int kc) { return (int)((n + kc - 1) / kc * kc); }
 
 template <typename T, int D, bool TR, int NTH = V2_THREADS>
 __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base, int64_t st, int64_t nrows,
@@ -574,15 +582,16 @@ __device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t 
     dst[i] = i < p.Lk ? (p.key_bias ? fmaxf(p.key_bias[b * p.Lk + i] * LOG2E, -1e30f) : 0.f) : -INFINITY;
 }
 
-template <int D, int HPB, bool REL>
+template <typename T, int D, int HPB, bool REL>
 __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
-  // domain) over 64-key chunks; key mask/padding come from a per-key bias vector in LDS.
+  // domain) over 64-key chunks (the last one holds only the padded key count's subtiles); key
+  // mask/padding come from a per-key bias vector in LDS.
   // HPB > 1 (short windows: Lq <= 64 / 32, Lk <= 64, e.g. Swinv2's 8x8 windows): the 8 waves split
   // into HPB groups, each owning one (b, h) with its own LDS images, so no wave idles on a head
   // that has fewer 16-query blocks than the workgroup has waves.
-  using T = bf16;
   using C = AT<T, D>;
+  constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
   constexpr int WPH = (V2_THREADS / 64) / HPB;  // waves per head
   constexpr int TPH = V2_THREADS / HPB;         // threads per head
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -592,17 +601,19 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   const int64_t nbh = p.B * p.H, bh_raw = (int64_t)blockIdx.x * HPB + sub;
   const bool active = bh_raw < nbh;
   const int64_t bh = active ? bh_raw : nbh - 1, b = bh / p.H, h = bh % p.H;
-  const int lk_pad = (int)((p.Lk + 63) & ~63);
+  const int lk_pad = v2_pad(p.Lk, KC);
   char* hbase = smem + sub * (2 * lk_pad * C::RB + lk_pad * 4);
   char* k_img = hbase;
   char* v_img = hbase + lk_pad * C::RB;
   float* kbias = reinterpret_cast<float*>(hbase + 2 * lk_pad * C::RB);
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
-  const bool cosine = REL && p.cos_ls != nullptr;
-  if (cosine)
-    stage_rows_cos<D, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
-  else
-    stage_all<T, D, false, TPH>(k_img, reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk, lk_pad, htid, p.D);
+  const T* kb_g = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  bool cosine = false;
+  if constexpr (sizeof(T) == 2) {
+    cosine = REL && p.cos_ls != nullptr;
+    if (cosine) stage_rows_cos<D, TPH>(k_img, kb_g, p.k_st, p.Lk, lk_pad, htid, p.D);
+  }
+  if (!cosine) stage_all<T, D, false, TPH>(k_img, kb_g, p.k_st, p.Lk, lk_pad, htid, p.D);
   stage_all<T, D, true, TPH>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, htid, p.D);
   stage_kbias<TPH>(kbias, p, b, lk_pad, htid);
   __syncthreads();
@@ -623,7 +634,9 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
     for (int kc = 0; kc < C::KCH; ++kc) qf[kc] = qn[kc];
     load_row_regs<T, D>(qn, qb, p.q_st, q0 + WPH * 16 + li, p.Lq, lane, p.D);
-    if (cosine) cos_norm_q<D>(qf, qmult);
+    if constexpr (sizeof(T) == 2) {
+      if (cosine) cos_norm_q<D>(qf, qmult);
+    }
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
@@ -631,18 +644,44 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < lk_pad; k0 += 64) {
+      const int nsub = min(4, (lk_pad - k0) >> 4);  // 16-key subtiles present in this chunk
       const char* kc_img = k_img + k0 * C::RB;
       const char* vc_img = v_img + k0 * C::RB;
       f32x4 s[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < 4; ++ks) s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (nsub == 4) {  // full chunk: four interleaved S^T chains, K fragments read one k-chunk ahead
+        uint4 fa[4], fb[4], fn[4];
 #pragma unroll
-        for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
+        for (int ks = 0; ks < 4; ++ks) { fa[ks] = row_frag<T, D>(kc_img, ks, 0, lane); fb[ks] = qf[0]; }
+#pragma unroll
+        for (int kc = 0; kc < C::KCH; ++kc) {
+          if (kc + 1 < C::KCH) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) fn[ks] = row_frag<T, D>(kc_img, ks, kc + 1, lane);
+          }
+          Mma<T>::template runN<4>(s, fa, fb);
+          if (kc + 1 < C::KCH) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) { fa[ks] = fn[ks]; fb[ks] = qf[kc + 1]; }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          if (ks < nsub) {
+#pragma unroll
+            for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
+          }
+        }
       }
       float mx = -INFINITY;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
+        if (ks >= nsub) {
+          s[ks] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+          continue;
+        }
         const float4 kb4 = *reinterpret_cast<const float4*>(kbias + k0 + ks * 16 + 4 * g);
         const float kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
         float rb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -672,7 +711,8 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float rs = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks >= nsub) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(s[ks][r] - mnew);
@@ -684,6 +724,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
           }
           s[ks][r] = pe;
         }
+      }
       lsum = lsum * alpha + rs;  // per-lane partial over this lane's keys; reduced at the end
       m = mnew;
 #pragma unroll
@@ -693,10 +734,13 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
         for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
       }
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < 4 / SUBS; ++c) {
+        if (c * SUBS >= nsub) continue;
+        uint4 fa[C::DT], fb[C::DT];
         const uint4 a = pack_acc<T>(s, c);
 #pragma unroll
-        for (int d = 0; d < C::DT; ++d) Mma<T>::run(o[d], a, tr_frag<T, D>(vc_img, c, d, lane));
+        for (int d = 0; d < C::DT; ++d) { fa[d] = a; fb[d] = tr_frag<T, D>(vc_img, c, d, lane); }
+        Mma<T>::template runN<C::DT>(o, fa, fb);
       }
     }
     lsum += __shfl_xor(lsum, 16, 64);
@@ -716,18 +760,18 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   }
 }
 
-template <int D>
-__global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) {
+template <typename T, int D, int NTH>
+__global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   // Q/dO of the head resident in LDS (plus lse, delta in log2 units); each wave owns 16 keys
-  using T = bf16;
   using C = AT<T, D>;
+  constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const int lq_pad = (int)((p.Lq + 31) & ~31);
+  const int lq_pad = v2_pad(p.Lq, KC);
   const int img = lq_pad * C::RB;
-  constexpr bool DUAL = V2<D>::DUAL;
+  constexpr bool DUAL = V2<T, D>::DUAL;
   char* q_row = smem;
   char* do_row = smem + img;
   char* q_tr = DUAL ? q_row : smem + 2 * img;
@@ -737,15 +781,15 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   float* kbias = s_delta + V2_LMAX;
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
-  stage_all<T, D, false, V2_DKDV_THREADS>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  if (!DUAL) stage_all<T, D, true, V2_DKDV_THREADS>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, false, V2_DKDV_THREADS>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  if (!DUAL) stage_all<T, D, true, V2_DKDV_THREADS>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  for (int i = tid; i < lq_pad; i += V2_DKDV_THREADS) {
+  stage_all<T, D, false, NTH>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true, NTH>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
+  stage_all<T, D, false, NTH>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true, NTH>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  for (int i = tid; i < lq_pad; i += NTH) {
     s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] * LOG2E : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
   }
-  stage_kbias<V2_DKDV_THREADS>(kbias, p, b, (int)((p.Lk + 15) & ~15), tid);
+  stage_kbias<NTH>(kbias, p, b, (int)((p.Lk + 15) & ~15), tid);
   __syncthreads();
   const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
   const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
@@ -755,28 +799,57 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
   const int nkb = (int)((p.Lk + 15) / 16);
-  const int nqc = lq_pad / 32;  // 32-query chunks
-  for (int kbk = wave; kbk < nkb; kbk += V2_DKDV_THREADS / 64) {
+  const int nqc = lq_pad / KC;  // query chunks of one MFMA k-chunk
+  for (int kbk = wave; kbk < nkb; kbk += NTH / 64) {
     const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
     uint4 kf[C::KCH], vf[C::KCH];
     load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
     load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
     const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
-    f32x4 dk[C::DT], dv[C::DT];
+    f32x4 dkv[2 * C::DT];  // dV (even) and dK (odd) of each 16-wide D subtile
 #pragma unroll
-    for (int d = 0; d < C::DT; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+    for (int i = 0; i < 2 * C::DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Q / dO row fragments of the first query chunk; each iteration prefetches the next chunk's
+    uint4 qa[SUBS * C::KCH], da[SUBS * C::KCH];
+#pragma unroll
+    for (int i = 0; i < SUBS * C::KCH; ++i) {
+      qa[i] = row_frag<T, D>(q_row, i / C::KCH, i % C::KCH, lane);
+      da[i] = row_frag<T, D>(do_row, i / C::KCH, i % C::KCH, lane);
+    }
     for (int qc = 0; qc < nqc; ++qc) {
-      f32x4 pd[2], ds[2];
+      // transposed dO / Q fragments of this chunk (B operands of dV / dK), read ahead of the softmax
+      uint4 tb[2 * C::DT];
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int qs = 2 * qc + h2;
-        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+      for (int d = 0; d < C::DT; ++d) {
+        tb[2 * d] = tr_frag<T, D>(do_tr, qc, d, lane);
+        tb[2 * d + 1] = tr_frag<T, D>(q_tr, qc, d, lane);
+      }
+      f32x4 sd[2 * SUBS];  // S (even) and dP (odd) of each 16-query subtile, interleaved chains
 #pragma unroll
-        for (int kc = 0; kc < C::KCH; ++kc) {
-          Mma<T>::run(sv, row_frag<T, D>(q_row, qs, kc, lane), kf[kc]);
-          Mma<T>::run(dp, row_frag<T, D>(do_row, qs, kc, lane), vf[kc]);
+      for (int i = 0; i < 2 * SUBS; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) {
+        uint4 fa[2 * SUBS], fb[2 * SUBS];
+#pragma unroll
+        for (int h2 = 0; h2 < SUBS; ++h2) {
+          fa[2 * h2] = qa[h2 * C::KCH + kc]; fb[2 * h2] = kf[kc];
+          fa[2 * h2 + 1] = da[h2 * C::KCH + kc]; fb[2 * h2 + 1] = vf[kc];
         }
+        Mma<T>::template runN<2 * SUBS>(sd, fa, fb);
+      }
+      if (qc + 1 < nqc) {
+#pragma unroll
+        for (int i = 0; i < SUBS * C::KCH; ++i) {
+          qa[i] = row_frag<T, D>(q_row, SUBS * (qc + 1) + i / C::KCH, i % C::KCH, lane);
+          da[i] = row_frag<T, D>(do_row, SUBS * (qc + 1) + i / C::KCH, i % C::KCH, lane);
+        }
+      }
+      f32x4 pd[SUBS], ds[SUBS];
+#pragma unroll
+      for (int h2 = 0; h2 < SUBS; ++h2) {
+        const int qs = SUBS * qc + h2;
+        const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
         const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qs * 16 + 4 * g);
         const float4 d4 = *reinterpret_cast<const float4*>(s_delta + qs * 16 + 4 * g);
         const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
@@ -797,11 +870,10 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
       }
       const uint4 ap = pack_acc<T>(pd, 0);
       const uint4 as = pack_acc<T>(ds, 0);
+      uint4 fa[2 * C::DT];
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) {
-        Mma<T>::run(dv[d], ap, tr_frag<T, D>(do_tr, qc, d, lane));
-        Mma<T>::run(dk[d], as, tr_frag<T, D>(q_tr, qc, d, lane));
-      }
+      for (int d = 0; d < C::DT; ++d) { fa[2 * d] = ap; fa[2 * d + 1] = as; }
+      Mma<T>::template runN<2 * C::DT>(dkv, fa, tb);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -812,7 +884,7 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
           if (d * 16 + li >= p.D) continue;
           T* pk = dkb + key * p.dk_st + d * 16 + li;
           T* pv = dvb + key * p.dv_st + d * 16 + li;
-          float vk = dk[d][r] * p.scale, vv = dv[d][r];
+          float vk = dkv[2 * d + 1][r] * p.scale, vv = dkv[2 * d][r];
           if (p.acc_dkv) { vk += to_f32(*pk); vv += to_f32(*pv); }
           *pk = from_f32<T>(vk);
           *pv = from_f32<T>(vv);
@@ -822,18 +894,18 @@ __global__ void __launch_bounds__(V2_DKDV_THREADS) attn_dkdv_v2_kernel(AttnP p) 
   }
 }
 
-template <int D>
+template <typename T, int D>
 __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K
-  using T = bf16;
   using C = AT<T, D>;
+  constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const int lk_pad = (int)((p.Lk + 31) & ~31);
+  const int lk_pad = v2_pad(p.Lk, KC);
   const int img = lk_pad * C::RB;
-  constexpr bool DUAL = V2<D>::DUAL;
+  constexpr bool DUAL = V2<T, D>::DUAL;
   char* k_row = smem;
   char* v_row = smem + img;
   char* k_tr = DUAL ? k_row : smem + 2 * img;
@@ -851,7 +923,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
-  const int nkc = lk_pad / 32;
+  const int nkc = lk_pad / KC;
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH], dof[C::KCH];
@@ -864,17 +936,42 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K / V row fragments of the first key chunk; each iteration prefetches the next chunk's
+    uint4 ka[SUBS * C::KCH], va[SUBS * C::KCH];
+#pragma unroll
+    for (int i = 0; i < SUBS * C::KCH; ++i) {
+      ka[i] = row_frag<T, D>(k_row, i / C::KCH, i % C::KCH, lane);
+      va[i] = row_frag<T, D>(v_row, i / C::KCH, i % C::KCH, lane);
+    }
     for (int kc2 = 0; kc2 < nkc; ++kc2) {
-      f32x4 ds[2];
+      uint4 tk[C::DT];  // transposed K fragments (B operand of dQ), read ahead of the softmax
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int ks = 2 * kc2 + h2;
-        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = sv;
+      for (int d = 0; d < C::DT; ++d) tk[d] = tr_frag<T, D>(k_tr, kc2, d, lane);
+      f32x4 sd[2 * SUBS];
 #pragma unroll
-        for (int kc = 0; kc < C::KCH; ++kc) {
-          Mma<T>::run(sv, row_frag<T, D>(k_row, ks, kc, lane), qf[kc]);
-          Mma<T>::run(dp, row_frag<T, D>(v_row, ks, kc, lane), dof[kc]);
+      for (int i = 0; i < 2 * SUBS; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) {
+        uint4 fa[2 * SUBS], fb[2 * SUBS];
+#pragma unroll
+        for (int h2 = 0; h2 < SUBS; ++h2) {
+          fa[2 * h2] = ka[h2 * C::KCH + kc]; fb[2 * h2] = qf[kc];
+          fa[2 * h2 + 1] = va[h2 * C::KCH + kc]; fb[2 * h2 + 1] = dof[kc];
         }
+        Mma<T>::template runN<2 * SUBS>(sd, fa, fb);
+      }
+      if (kc2 + 1 < nkc) {
+#pragma unroll
+        for (int i = 0; i < SUBS * C::KCH; ++i) {
+          ka[i] = row_frag<T, D>(k_row, SUBS * (kc2 + 1) + i / C::KCH, i % C::KCH, lane);
+          va[i] = row_frag<T, D>(v_row, SUBS * (kc2 + 1) + i / C::KCH, i % C::KCH, lane);
+        }
+      }
+      f32x4 ds[SUBS];
+#pragma unroll
+      for (int h2 = 0; h2 < SUBS; ++h2) {
+        const int ks = SUBS * kc2 + h2;
+        const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
         const float4 kb4 = *reinterpret_cast<const float4*>(kbias + ks * 16 + 4 * g);
         const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
 #pragma unroll
@@ -892,8 +989,10 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
         }
       }
       const uint4 as = pack_acc<T>(ds, 0);
+      uint4 fa[C::DT];
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) Mma<T>::run(dq[d], as, tr_frag<T, D>(k_tr, kc2, d, lane));
+      for (int d = 0; d < C::DT; ++d) fa[d] = as;
+      Mma<T>::template runN<C::DT>(dq, fa, tk);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -951,62 +1050,61 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   return 0;
 }
 
-template <int D>
 void set_lds_attr(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-template <int D, int HPB, bool REL>
+template <typename T, int D, int HPB, bool REL>
 void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
-  const int lk_pad = (int)((p.Lk + 63) & ~63);
-  const int lds = HPB * (2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4);
-  constexpr int lmax = HPB == 1 ? V2_LMAX_FWD : 64;
-  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<D, HPB, REL>),
-                                      HPB * (2 * lmax * AT<bf16, D>::RB + lmax * 4)), true);
+  constexpr int RB = AT<T, D>::RB;
+  const int lk_pad = v2_pad(p.Lk, v2_kc<T>());
+  const int lds = HPB * (2 * lk_pad * RB + lk_pad * 4);
+  constexpr int lmax = HPB == 1 ? (sizeof(T) == 2 ? V2_LMAX_FWD : V2_LMAX) : 64;
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<T, D, HPB, REL>),
+                                   HPB * (2 * lmax * RB + lmax * 4)), true);
   (void)once;
   const int64_t nbh = p.B * p.H;
-  hipLaunchKernelGGL((attn_fwd_v2_kernel<D, HPB, REL>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS), lds,
-                     s, p);
+  hipLaunchKernelGGL((attn_fwd_v2_kernel<T, D, HPB, REL>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS),
+                     lds, s, p);
 }
 
 // the relative-bias instantiation carries the extra loads / registers; plain attention (BERT, ViT,
 // fusion head) keeps the bias-free one
-template <int D, int HPB>
+template <typename T, int D, int HPB>
 void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
   if (p.rel_bias)
-    launch_fwd_v2_hpb<D, HPB, true>(p, s);
+    launch_fwd_v2_hpb<T, D, HPB, true>(p, s);
   else
-    launch_fwd_v2_hpb<D, HPB, false>(p, s);
+    launch_fwd_v2_hpb<T, D, HPB, false>(p, s);
 }
 
-template <int D>
+template <typename T, int D>
 void launch_fwd_v2(const AttnP& p, hipStream_t s) {
   // short windows: several heads per workgroup so all 8 waves own a 16-query block
   if (p.Lk <= 64 && p.Lq <= 32)
-    launch_fwd_v2_hpb<D, 4>(p, s);
+    launch_fwd_v2_hpb<T, D, 4>(p, s);
   else if (p.Lk <= 64 && p.Lq <= 64)
-    launch_fwd_v2_hpb<D, 2>(p, s);
+    launch_fwd_v2_hpb<T, D, 2>(p, s);
   else
-    launch_fwd_v2_hpb<D, 1>(p, s);
+    launch_fwd_v2_hpb<T, D, 1>(p, s);
 }
 
-template <int D>
+template <typename T, int D>
 void launch_bwd_v2(const AttnP& p, hipStream_t s) {
   const int64_t rows = p.B * p.H * p.Lq;
-  constexpr int nch = AT<bf16, D>::NCH;
-  hipLaunchKernelGGL((attn_delta_kernel<bf16, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
-  const int lq_pad = (int)((p.Lq + 31) & ~31), lk_pad = (int)((p.Lk + 31) & ~31);
-  constexpr int NI1 = V2<D>::DUAL ? 2 : 4, NI2 = V2<D>::DUAL ? 2 : 3;  // LDS images per kernel
-  const int lds1 = NI1 * lq_pad * AT<bf16, D>::RB + 3 * V2_LMAX * 4;
-  const int lds2 = NI2 * lk_pad * AT<bf16, D>::RB + lk_pad * 4;
-  static bool once = (set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<D>),
-                                      NI1 * V2_LMAX * AT<bf16, D>::RB + 3 * V2_LMAX * 4),
-                      set_lds_attr<D>(reinterpret_cast<const void*>(&attn_dq_v2_kernel<D>),
-                                      NI2 * V2_LMAX * AT<bf16, D>::RB + V2_LMAX * 4),
+  constexpr int nch = AT<T, D>::NCH, RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
+  hipLaunchKernelGGL((attn_delta_kernel<T, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
+  const int lq_pad = v2_pad(p.Lq, v2_kc<T>()), lk_pad = v2_pad(p.Lk, v2_kc<T>());
+  constexpr int NI1 = V2<T, D>::DUAL ? 2 : 4, NI2 = V2<T, D>::DUAL ? 2 : 3;  // LDS images per kernel
+  const int lds1 = NI1 * lq_pad * RB + 3 * V2_LMAX * 4;
+  const int lds2 = NI2 * lk_pad * RB + lk_pad * 4;
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH>),
+                                   NI1 * V2_LMAX * RB + 3 * V2_LMAX * 4),
+                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D>), NI2 * V2_LMAX * RB + V2_LMAX * 4),
                       true);
   (void)once;
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_DKDV_THREADS), lds1, s, p);
-  hipLaunchKernelGGL((attn_dq_v2_kernel<D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
+  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
 }
 
 template <typename T, int D>
@@ -1040,11 +1138,13 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   // one workgroup per (b, h): past 256 keys only when there are enough heads to fill the chip (a
   // batch-1 pair at L = 512 runs faster on the 64-query-block streaming kernel)
-  const bool v2 = a->dtype == MMFD_BF16 && (p.Lk <= V2_LMAX || (p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) &&
-                  !getenv("MMFD_ATTN_V1");
-  MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && a->rel_bias),
-                 "attn_fwd: cosine attention needs the bf16 resident-K/V kernel (Lk <= 256) and a rel_bias");
-  if (v2) { if (a->D > 32) launch_fwd_v2<64>(p, s); else launch_fwd_v2<32>(p, s); }
+  // (fp32 K/V images of 512 keys would not fit the LDS)
+  const bool bf = a->dtype == MMFD_BF16;
+  const bool v2 = (p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !getenv("MMFD_ATTN_V1");
+  MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && bf && a->rel_bias),
+                 "attn_fwd: cosine attention needs bf16, the resident-K/V kernel (Lk <= 256) and a rel_bias");
+  if (v2 && bf) { if (a->D > 32) launch_fwd_v2<bf16, 64>(p, s); else launch_fwd_v2<bf16, 32>(p, s); }
+  else if (v2) { if (a->D > 32) launch_fwd_v2<float, 64>(p, s); else launch_fwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_fwd");
@@ -1058,8 +1158,9 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const bool v2 = a->dtype == MMFD_BF16 && p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1");
-  if (v2) { if (a->D > 32) launch_bwd_v2<64>(p, s); else launch_bwd_v2<32>(p, s); }
+  const bool v2 = p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  if (v2 && a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd_v2<bf16, 64>(p, s); else launch_bwd_v2<bf16, 32>(p, s); }
+  else if (v2) { if (a->D > 32) launch_bwd_v2<float, 64>(p, s); else launch_bwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_bwd");

@@ -134,6 +134,12 @@ template <> struct Mma<bf16> {
     bf16x8 bv = __builtin_bit_cast(bf16x8, b);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
   }
+  // N independent accumulators, one chunk each
+  template <int N>
+  __device__ __forceinline__ static void runN(f32x4* acc, const uint4* a, const uint4* b) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) run(acc[i], a[i], b[i]);
+  }
 };
 template <> struct Mma<float> {
   static constexpr int KC = 16;
@@ -142,6 +148,23 @@ template <> struct Mma<float> {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+  // N independent accumulators with their k-steps interleaved: back to back, one chain's 16x16x4
+  // MFMAs would wait out the 40-cycle dependent latency instead of the 32-cycle issue
+  template <int N>
+  __device__ __forceinline__ static void runN(f32x4* acc, const uint4* a, const uint4* b) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].x), __uint_as_float(b[i].x), acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].y), __uint_as_float(b[i].y), acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].z), __uint_as_float(b[i].z), acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].w), __uint_as_float(b[i].w), acc[i], 0, 0, 0);
   }
 };
 

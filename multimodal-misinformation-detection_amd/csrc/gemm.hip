@@ -497,6 +497,23 @@ __device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2
   __builtin_amdgcn_s_setprio(0);
 }
 
+// two quadrants sharing the A fragments (one phase of the two-phase schedule)
+template <typename T>
+__device__ __forceinline__ void g8_mma2(f32x4 (&acc0)[4][2], f32x4 (&acc1)[4][2], const uint4 (&a)[4][2],
+                                        const uint4 (&b0)[2][2], const uint4 (&b1)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        Mma<T>::run(acc0[i][j], b0[j][kc], a[i][kc]);
+        Mma<T>::run(acc1[i][j], b1[j][kc], a[i][kc]);
+      }
+  __builtin_amdgcn_s_setprio(0);
+}
+
 template <typename T>
 __device__ __forceinline__ float g8_sum16b(uint4 x) {  // the elements of one 16-B chunk
   if (sizeof(T) == 4)
@@ -586,7 +603,17 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     }
   };
 
-  if (nk > 0) {
+  constexpr bool PH2 = sizeof(T) == 2;  // bf16: two-phase schedule (see the main loop)
+  if (PH2 && nk > 0) {
+    // two-phase schedule: A-h0, B-h0, B-h1 of K-tile t are read in phase X(t), A-h1 in phase Y(t)
+    issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0);
+    if (nk > 1) {
+      issue(0, 1); issue(2, 1); issue(3, 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else if (nk > 0) {
     issue(0, 0); issue(3, 0); issue(1, 0); issue(2, 0);
     if (nk > 1) {
       issue(0, 1); issue(3, 1); issue(1, 1);
@@ -604,40 +631,81 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   float rs0 = 0.f, rs1 = 0.f;
 
   uint4 fa[4][2], fb[2][2];
-  for (int t = 0; t < nk; ++t) {
-    // phase 0: quadrant (0,0)
-    g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
-    g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
-    if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
-    if (t + 1 < nk) issue(2, t + 1);
-    g8_pre_barrier();
-    g8_mma<T>(acc[0][0], fa, fb);
-    g8_barrier();
-    // phase 1: quadrant (0,1)
-    g8_frag_b<T, TB>(fb, img(t, 3), wc, lane);
-    if (t + 2 < nk) issue(0, t + 2);
-    g8_pre_barrier();
-    g8_mma<T>(acc[0][1], fa, fb);
-    g8_barrier();
-    // phase 2: quadrant (1,1)
-    g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
-    if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
-    if (t + 2 < nk) issue(3, t + 2);
-    g8_pre_barrier();
-    g8_mma<T>(acc[1][1], fa, fb);
-    g8_barrier();
-    // phase 3: quadrant (1,0); K-tile t+1 must have landed before the next phase reads it
-    g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
-    if (t + 2 < nk) {
-      issue(1, t + 2);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (PH2) {
+    // Two phases per K-tile, 32 MFMAs each (one quadrant per phase, as fp32 below, measured 3.5 %
+    // slower over the encoder shapes: twice the barrier hand-offs): X(t) = quadrants (0,0), (0,1)
+    // from A-h0 and both B halves; Y(t) = quadrants (1,0), (1,1) from A-h1 with the B fragments
+    // kept in registers. Refills: X(t) issues A-h1 of
+    // t+1 (last read in Y(t-1)), Y(t) issues A-h0 / B-h0 / B-h1 of t+2 (last read in X(t)); each
+    // phase then waits until at most the 8 pieces issued after the next phase's operands remain.
+    uint4 fbh[2][2];
+    for (int t = 0; t < nk; ++t) {
+      // phase X(t)
+      g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
+      g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
+      g8_frag_b<T, TB>(fbh, img(t, 3), wc, lane);
+      if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (t + 1 < nk) {
+        issue(1, t + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      g8_pre_barrier();
+      g8_mma2<T>(acc[0][0], acc[0][1], fa, fb, fbh);
+      g8_barrier();
+      // phase Y(t)
+      g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
+      if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (t + 2 < nk) {
+        issue(0, t + 2); issue(2, t + 2); issue(3, t + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      g8_pre_barrier();
+      g8_mma2<T>(acc[1][0], acc[1][1], fa, fb, fbh);
+      g8_barrier();
     }
-    g8_pre_barrier();
-    g8_mma<T>(acc[1][0], fa, fb);
-    g8_barrier();
+  } else {
+    // fp32: four phases of one quadrant each (the two-phase schedule pushes the fp32 layout-1
+    // fragment addressing past 256 VGPRs into scratch and measured no faster)
+    for (int t = 0; t < nk; ++t) {
+      // phase 0: quadrant (0,0)
+      g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
+      g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
+      if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (t + 1 < nk) issue(2, t + 1);
+      g8_pre_barrier();
+      g8_mma<T>(acc[0][0], fa, fb);
+      g8_barrier();
+      // phase 1: quadrant (0,1)
+      g8_frag_b<T, TB>(fb, img(t, 3), wc, lane);
+      if (t + 2 < nk) issue(0, t + 2);
+      g8_pre_barrier();
+      g8_mma<T>(acc[0][1], fa, fb);
+      g8_barrier();
+      // phase 2: quadrant (1,1)
+      g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
+      if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (t + 2 < nk) issue(3, t + 2);
+      g8_pre_barrier();
+      g8_mma<T>(acc[1][1], fa, fb);
+      g8_barrier();
+      // phase 3: quadrant (1,0); K-tile t+1 must have landed before the next phase reads it
+      g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
+      if (t + 2 < nk) {
+        issue(1, t + 2);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      g8_pre_barrier();
+      g8_mma<T>(acc[1][0], fa, fb);
+      g8_barrier();
+    }
   }
+
   G8_STAMP(1);
   if (wr == 0) g8_barrier();  // re-align the wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

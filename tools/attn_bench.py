@@ -12,13 +12,13 @@ import mmfd  # noqa: E402
 from mmfd import kernels as K  # noqa: E402
 
 
-def case(name, L, masked, p, iters):
+def case(name, L, masked, p, iters, dtype=torch.bfloat16):
     B, H, D = 512, 12, 64
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(0)
-    qkv = torch.randn(B, L, 3 * H * D, generator=g).to(dev, torch.bfloat16)
+    qkv = torch.randn(B, L, 3 * H * D, generator=g).to(dev, dtype)
     q, k, v = qkv[..., :H * D], qkv[..., H * D:2 * H * D], qkv[..., 2 * H * D:]
-    dout = torch.randn(B, L, H * D, generator=g).to(dev, torch.bfloat16)
+    dout = torch.randn(B, L, H * D, generator=g).to(dev, dtype)
     kb = None
     if masked:
         mask = torch.ones(B, L, dtype=torch.long)
@@ -53,8 +53,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--dtype", default="bf16,fp32")
     a = ap.parse_args()
-    if a.only in ("", "bert"):
-        case("bert L=128 mask+drop", 128, True, 0.1, a.iters)
-    if a.only in ("", "vit"):
-        case("vit  L=197          ", 197, False, 0.0, a.iters)
+    for dt in a.dtype.split(","):
+        t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
+        if a.only in ("", "bert"):
+            case(f"{dt} bert L=128 mask+drop", 128, True, 0.1, a.iters, t)
+        if a.only in ("", "vit"):
+            case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t)

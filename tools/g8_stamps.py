@@ -2,7 +2,7 @@
 -DMMFD_G8_STAMPS build of libmmfd_hip under tools/_stamps/; the product library is untouched).
 Stamps: 0 start, 1 mainloop done, 2 after the re-align + vmcnt(0) + barrier, 3 staging written,
 4 after the staging barrier, 5 first 128 rows read back + stored, 6 epilogue issued, 7 stores
-retired (vmcnt(0)).   python tools/g8_stamps.py [M N K [plain|gelu|gelubwd]]"""
+retired (vmcnt(0)).   python tools/g8_stamps.py [M N K [plain|gelu|gelubwd] [bf16|fp32]]"""
 import ctypes
 import os
 import subprocess
@@ -34,11 +34,12 @@ lib = K.lib()
 lib.mmfd_debug_g8_stamps.restype = ctypes.c_int
 lib.mmfd_debug_g8_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 M, N, Kd = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (65536, 3072, 768)
-A = torch.randn(M, Kd, device="cuda").bfloat16()
-B = torch.randn(N, Kd, device="cuda").bfloat16()
-out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 kind = sys.argv[4] if len(sys.argv) > 4 else "plain"
-aux = torch.randn(M, N, device="cuda").bfloat16()
+dt = torch.float32 if (len(sys.argv) > 5 and sys.argv[5] == "fp32") else torch.bfloat16
+A = torch.randn(M, Kd, device="cuda").to(dt)
+B = torch.randn(N, Kd, device="cuda").to(dt)
+out = torch.empty(M, N, device="cuda", dtype=dt)
+aux = torch.randn(M, N, device="cuda").to(dt)
 bias = torch.randn(N, device="cuda")
 for _ in range(5):
     if kind == "gelu":
