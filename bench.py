@@ -601,7 +601,8 @@ def main():
                                                   "preembed", "preembed_image"],
                     default="train")
     ap.add_argument("--no-bf16", action="store_true", help="skip the secondary bf16 leg of the fp32 headline")
-    ap.add_argument("--graph", action="store_true", help="time HIP-graph replays of the captured step (experimental)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eager steps instead of HIP-graph replays of the captured step (N = 1)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -690,7 +691,7 @@ def train_leg(args, dev, world, rank, precision):
     tr = build_flagship(dev, precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42, rank=rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 
-    graphed = world == 1 and args.graph
+    graphed = world == 1 and not args.no_graph
     probe = K.GemmProbe()
     if graphed:  # the whole step as one HIP graph (capture runs its own eager warmup steps first)
         tr.capture(batch, warmup=max(1, args.warmup))

@@ -68,11 +68,24 @@ class AdamW(torch.optim.Optimizer):
     # ---- HIP-graph capture: the pointer table is late-bound ------------------------------------------
     # Under stream capture the gradients are fresh graph-pool tensors whose table cannot be uploaded
     # from the host (no synchronous copies while capturing). The captured launch reads a device table
-    # reserved here; finalize_capture() fills it once the captured step has assigned every .grad
-    # (the same tensors every replay writes).
-    def _capture_table(self, entries):
-        n = len(entries) * ctypes.sizeof(K.AdamWTensor)
-        t = torch.empty(n, dtype=torch.uint8, device=entries[0][0].device)
+    # that prepare_capture() reserved BEFORE the capture: a table allocated inside the capture would
+    # come from the graph's private pool, where it may share bytes with temporaries that earlier
+    # kernels of the same graph write at every replay (the host-written pointers would be clobbered
+    # before the AdamW launch reads them). finalize_capture() fills the reserved tables once the
+    # captured step has assigned every .grad (the same tensors every replay writes).
+    def prepare_capture(self):
+        dev = next(p.device for g in self.param_groups for p in g["params"])
+        self._reserved = [torch.empty(max(1, len(g["params"])) * ctypes.sizeof(K.AdamWTensor), dtype=torch.uint8,
+                                      device=dev) for g in self.param_groups]
+        self._pending_capture = []
+
+    def _capture_table(self, gi, entries):
+        res = getattr(self, "_reserved", None)
+        if res is None:
+            raise RuntimeError("mmfd AdamW: call prepare_capture() before capturing a step in a HIP graph")
+        t = res[gi]
+        if t.numel() < len(entries) * ctypes.sizeof(K.AdamWTensor):
+            raise RuntimeError("mmfd AdamW: reserved capture table too small")
         self._pending_capture = getattr(self, "_pending_capture", []) + [(t, entries)]
         return t
 
@@ -88,10 +101,11 @@ class AdamW(torch.optim.Optimizer):
                 arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
                 arr[i].param_bf16 = sh[0].data_ptr() if ok else None
                 arr[i].step, arr[i].numel = st.data_ptr(), p.numel()
-            t.copy_(torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8))
+            t[: ctypes.sizeof(arr)].copy_(torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8))
         # the captured launches read these tables at every replay: keep them alive with the graph
         self._captured_tables = getattr(self, "_captured_tables", []) + [t for t, _ in self._pending_capture]
         self._pending_capture = []
+        self._reserved = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -99,7 +113,7 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             entries = []
             for p in group["params"]:
                 if p.grad is None:
@@ -120,7 +134,7 @@ class AdamW(torch.optim.Optimizer):
                 continue
             b1, b2 = group["betas"]
             if torch.cuda.is_current_stream_capturing():
-                table = self._capture_table(entries)
+                table = self._capture_table(gi, entries)
             else:
                 table = self._table(entries, entries[0][0].device)
             K.adamw(table, len(entries), max(e[0].numel() for e in entries), group["lr"], b1, b2, group["eps"],

@@ -174,6 +174,7 @@ class FusionTrainer:
             for _ in range(warmup):  # optimizer state, weight shadows, kernel attributes
                 self.step(batch)
         torch.cuda.current_stream().wait_stream(s)
+        self.optimizer.prepare_capture()  # pointer tables outside the graph's memory pool
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._graph_loss = self.step(batch)
