@@ -760,9 +760,11 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D, int NTH>
+template <typename T, int D, int NTH, bool REL>
 __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
-  // Q/dO of the head resident in LDS (plus lse, delta in log2 units); each wave owns 16 keys
+  // Q/dO of the head resident in LDS (plus lse, delta in log2 units); each wave owns 16 keys.
+  // REL: the additive [H][Lq][Lk] bias (MPNet / DeBERTa) — its loads and batch-modulus address
+  // math stay out of the bias-free instantiation (BERT, ViT, fusion head)
   using C = AT<T, D>;
   constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -807,6 +809,7 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
     load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
     const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
+    const float* relcol = REL ? p.rel_bias + rb_off(p, b) + h * p.Lq * p.Lk + (mykey < p.Lk ? mykey : 0) : nullptr;
     f32x4 dkv[2 * C::DT];  // dV (even) and dK (odd) of each 16-wide D subtile
 #pragma unroll
     for (int i = 0; i < 2 * C::DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -857,7 +860,7 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) {
           const int lq = qs * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kb2);
-          if (p.rel_bias && lq < p.Lq && mykey < p.Lk) t = fmaf(p.rel_bias[rb_off(p, b) + (h * p.Lq + lq) * p.Lk + mykey], LOG2E, t);
+          if (REL && lq < p.Lq && mykey < p.Lk) t = fmaf(relcol[(int64_t)lq * p.Lk], LOG2E, t);
           const float pr = __builtin_amdgcn_exp2f(t - lq2[r]);
           float z = 1.f;
           if (p.p > 0.f) {
@@ -894,9 +897,9 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D>
+template <typename T, int D, bool REL>
 __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
-  // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K
+  // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K (REL as in dK/dV)
   using C = AT<T, D>;
   constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -932,7 +935,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
     const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
-    const float* relrow = p.rel_bias ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
+    const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -978,7 +981,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) {
           const int key = ks * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kbr[r]);
-          if (relrow && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
+          if (REL && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
           const float pr = __builtin_amdgcn_exp2f(t - lse2);
           float z = 1.f;
           if (p.p > 0.f) {
@@ -1089,8 +1092,8 @@ void launch_fwd_v2(const AttnP& p, hipStream_t s) {
     launch_fwd_v2_hpb<T, D, 1>(p, s);
 }
 
-template <typename T, int D>
-void launch_bwd_v2(const AttnP& p, hipStream_t s) {
+template <typename T, int D, bool REL>
+void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
   const int64_t rows = p.B * p.H * p.Lq;
   constexpr int nch = AT<T, D>::NCH, RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
   hipLaunchKernelGGL((attn_delta_kernel<T, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
@@ -1098,13 +1101,22 @@ void launch_bwd_v2(const AttnP& p, hipStream_t s) {
   constexpr int NI1 = V2<T, D>::DUAL ? 2 : 4, NI2 = V2<T, D>::DUAL ? 2 : 3;  // LDS images per kernel
   const int lds1 = NI1 * lq_pad * RB + 3 * V2_LMAX * 4;
   const int lds2 = NI2 * lk_pad * RB + lk_pad * 4;
-  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH>),
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH, REL>),
                                    NI1 * V2_LMAX * RB + 3 * V2_LMAX * 4),
-                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D>), NI2 * V2_LMAX * RB + V2_LMAX * 4),
+                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D, REL>),
+                                   NI2 * V2_LMAX * RB + V2_LMAX * 4),
                       true);
   (void)once;
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
-  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
+  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
+}
+
+template <typename T, int D>
+void launch_bwd_v2(const AttnP& p, hipStream_t s) {
+  if (p.rel_bias)
+    launch_bwd_v2_rel<T, D, true>(p, s);
+  else
+    launch_bwd_v2_rel<T, D, false>(p, s);
 }
 
 template <typename T, int D>
