@@ -709,9 +709,8 @@ def train_leg(args, dev, world, rank, precision):
         for _ in range(args.steps):
             loss = tr.replay()
     else:
-        with probe:
-            for _ in range(args.steps):
-                loss = tr.step(batch)
+        for _ in range(args.steps):
+            loss = tr.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -725,17 +724,17 @@ def train_leg(args, dev, world, rank, precision):
     pairs = args.batch * world * args.steps / elapsed
     loss_val = loss[0].item()
 
-    if graphed:
-        # per-GEMM device times: events cannot be timed inside a graph, so two more steps of the
-        # same trainer run eagerly with the probe (the same kernels on the same shapes)
-        steps_in_prof = 2
-        with probe:
-            for _ in range(steps_in_prof):
-                tr.step(batch)
-        prof = probe.summary()
-    else:
-        prof = probe.summary()
-        steps_in_prof = args.steps
+    # per-GEMM device times from two more eager steps of the same trainer after the timed region
+    # (events cannot be timed inside a graph), with the two encoders on ONE stream: in the timed
+    # step they overlap on two streams, which is faster overall but stretches each kernel's
+    # duration by the CUs the other stream holds — the roofline is a property of the kernel alone
+    steps_in_prof = 2
+    conc, tr.concurrent = tr.concurrent, False
+    with probe:
+        for _ in range(steps_in_prof):
+            tr.step(batch)
+    tr.concurrent = conc
+    prof = probe.summary()
     dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[precision]
@@ -745,10 +744,12 @@ def train_leg(args, dev, world, rank, precision):
     kinds = {k: {"launches_per_step": v["launches"] // steps_in_prof, "avg_us": round(1000.0 * v["ms"] / v["launches"], 1),
                  "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
              for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+    tr_conc = conc and tr.dp is None
     del tr, batch
     return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
-            "launch": ("one HIP graph per step (captured fwd + bwd + AdamW); GEMM times from 2 eager probe steps "
-                       "after the timed replays") if graphed else "eager kernel launches (GEMM times over the timed steps)",
+            "launch": (("one HIP graph per step (captured fwd + bwd + AdamW)" if graphed else "eager kernel launches")
+                       + ("; text / image encoders on two streams" if tr_conc else "")
+                       + "; GEMM times from 2 eager probe steps after the timed region, encoders serialized"),
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
             "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,

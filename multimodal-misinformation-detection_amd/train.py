@@ -96,6 +96,8 @@ class FusionTrainer:
         self.params = [p for m in trained for p in m.parameters()]
         self.optimizer = AdamW(self.params, lr=lr)
         self.dp = dp
+        # text / image encoders on two streams (single process; see _encode)
+        self.concurrent = os.environ.get("MMFD_SERIAL_ENCODERS") != "1"
         if dp is not None:
             # every replica starts from rank 0's weights (frozen encoders included: all ranks must
             # compute the same function), then the gradient all-reduce overlaps the backward pass
@@ -107,6 +109,39 @@ class FusionTrainer:
     def _device(self):
         return next(self.head.parameters()).device
 
+    def _side_stream(self, dev):
+        st = getattr(self, "_side", None)
+        if st is None or st.device != dev:
+            st = self._side = torch.cuda.Stream(device=dev)
+        return st
+
+    def _encode(self, batch, dev):
+        """(T, I): the text and image encoders on the stacked claim/evidence inputs (frozen ones
+        without autograd). In a single process the two encoders run on two HIP streams — they are
+        independent until the head, so one's MFMA main loops overlap the other's HBM-bound
+        epilogues, attention and LayerNorms and fill its last-round GEMM tiles; autograd runs each
+        encoder's backward on its forward stream and joins them before the optimizer."""
+        ids = batch["input_ids"].to(dev, non_blocking=True)
+        mask = batch["attention_mask"].to(dev, non_blocking=True)
+        pix = batch["pixel_values"].to(dev, non_blocking=True)
+        conc = self.concurrent and self.dp is None
+        main = torch.cuda.current_stream(dev)
+        if conc:
+            side = self._side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
+                    T = self.text_encoder(input_ids=ids, attention_mask=mask).last_hidden_state
+        else:
+            with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
+                T = self.text_encoder(input_ids=ids, attention_mask=mask).last_hidden_state
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_image):
+            I = self.image_encoder(pix).last_hidden_state
+        if conc:
+            main.wait_stream(side)
+            T.record_stream(main)
+        return T, I
+
     def features(self, batch):
         """(X_t, X_i, E_t, E_i) for the head: the batch's pre-computed embeddings, or the encoders
         on the stacked claim/evidence inputs (frozen ones without autograd)"""
@@ -115,11 +150,7 @@ class FusionTrainer:
             return tuple(batch[k].to(dev, non_blocking=True) for k in
                          ("claim_text_embeds", "claim_image_embeds", "doc_text_embeds", "doc_image_embeds"))
         B = batch["labels"].shape[0]
-        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
-            T = self.text_encoder(input_ids=batch["input_ids"].to(dev, non_blocking=True),
-                                  attention_mask=batch["attention_mask"].to(dev, non_blocking=True)).last_hidden_state
-        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_image):
-            I = self.image_encoder(batch["pixel_values"].to(dev, non_blocking=True)).last_hidden_state
+        T, I = self._encode(batch, dev)
         return T[:B], I[:B], T[B:], I[B:]
 
     def loss(self, outs, labels):
@@ -132,12 +163,7 @@ class FusionTrainer:
         gradients come back as one tensor per encoder"""
         if "claim_text_embeds" in batch or self.text_encoder is None or self.image_encoder is None:
             return self.head(*self.features(batch))
-        dev = self._device()
-        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_text):
-            T = self.text_encoder(input_ids=batch["input_ids"].to(dev, non_blocking=True),
-                                  attention_mask=batch["attention_mask"].to(dev, non_blocking=True)).last_hidden_state
-        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_image):
-            I = self.image_encoder(batch["pixel_values"].to(dev, non_blocking=True)).last_hidden_state
+        T, I = self._encode(batch, self._device())
         return self.head.forward_pairs(T, I, batch["labels"].shape[0])
 
     def step(self, batch, return_outputs=False):
