@@ -744,7 +744,7 @@ def train_leg(args, dev, world, rank, precision):
     kinds = {k: {"launches_per_step": v["launches"] // steps_in_prof, "avg_us": round(1000.0 * v["ms"] / v["launches"], 1),
                  "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
              for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
-    tr_conc = conc and tr.dp is None
+    tr_conc = conc
     del tr, batch
     return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
             "launch": (("one HIP graph per step (captured fwd + bwd + AdamW)" if graphed else "eager kernel launches")

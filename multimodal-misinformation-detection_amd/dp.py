@@ -7,6 +7,12 @@ backward of each encoder reports every layer's finished parameter gradients (Ste
 they are packed into ~32 MB fp32 buckets and each full bucket is all-reduced asynchronously on
 RCCL's stream while the next layers' backward kernels run on the compute stream. `finish()` waits
 for the outstanding buckets and writes the averages into the parameters' .grad.
+
+The two encoders run on two HIP streams (mmfd.train.FusionTrainer._encode), and autograd runs each
+encoder's backward on its forward's stream, so gradients become ready on two streams. Buckets are
+therefore kept per stream: a bucket is packed and handed to RCCL on the stream that produced its
+gradients (RCCL orders a collective after the CURRENT stream only), and the per-step order of the
+collectives is the host order of the backward calls, the same on every rank.
 """
 from __future__ import annotations
 
@@ -38,21 +44,27 @@ class GradAllReduce:
 
     # ---- per-step protocol ------------------------------------------------------------------------
     def begin(self):
-        self._pending, self._pending_n = [], 0
+        self._pending = {}  # stream key -> [pending (param, grad) list, element count]
         self._works = []
-        self._nbucket = 0
+        self._nbucket = {}
+
+    @staticmethod
+    def _stream_key(g):
+        return torch.cuda.current_stream(g.device).cuda_stream if g.is_cuda else None
 
     def ready(self, pairs):
-        """pairs: iterable of (parameter, finished fp32 gradient tensor)"""
+        """pairs: iterable of (parameter, finished fp32 gradient tensor), produced on the current stream"""
         if not self._active():
             return
         for p, g in pairs:
             if g is None:
                 continue
-            self._pending.append((p, g))
-            self._pending_n += g.numel()
-            if self._pending_n >= self.bucket_elems:
-                self._flush()
+            key = self._stream_key(g)
+            ent = self._pending.setdefault(key, [[], 0])
+            ent[0].append((p, g))
+            ent[1] += g.numel()
+            if ent[1] >= self.bucket_elems:
+                self._flush(key)
 
     def hook_for(self, model):
         """callable(names, grads) for StepCtx.grad_ready: maps parameter names of `model` to params"""
@@ -64,7 +76,10 @@ class GradAllReduce:
         installed, which may or may not be the one that was packed)"""
         if not self._active():
             return
-        self._flush()
+        # leftovers of every stream, packed on the calling stream: backward() has returned, so the
+        # calling stream is already ordered after every gradient it reads
+        for key in list(self._pending):
+            self._flush(key)
         world = dist.get_world_size(self.group)
         for w, items, buf in self._works:
             w.wait()
@@ -113,17 +128,16 @@ class GradAllReduce:
     def _active(self):
         return dist.is_initialized() and dist.get_world_size(self.group) > 1
 
-    def _flush(self):
-        if not self._pending:
+    def _flush(self, key):
+        items, n = self._pending.pop(key, [[], 0])
+        if not items:
             return
-        items, n = self._pending, self._pending_n
-        self._pending, self._pending_n = [], 0
-        i = self._nbucket
-        self._nbucket += 1
+        i = self._nbucket.get(key, 0)
+        self._nbucket[key] = i + 1
         dev = items[0][1].device
-        buf = self._bufs.get(i)
+        buf = self._bufs.get((key, i))
         if buf is None or buf.numel() < n or buf.device != dev:
-            buf = self._bufs[i] = torch.empty(max(n, self.bucket_elems), device=dev, dtype=torch.float32)
+            buf = self._bufs[(key, i)] = torch.empty(max(n, self.bucket_elems), device=dev, dtype=torch.float32)
         off = 0
         for _, g in items:
             self._pack(g, buf[off:off + g.numel()])

@@ -96,7 +96,7 @@ class FusionTrainer:
         self.params = [p for m in trained for p in m.parameters()]
         self.optimizer = AdamW(self.params, lr=lr)
         self.dp = dp
-        # text / image encoders on two streams (single process; see _encode)
+        # text / image encoders on two streams (see _encode)
         self.concurrent = os.environ.get("MMFD_SERIAL_ENCODERS") != "1"
         if dp is not None:
             # every replica starts from rank 0's weights (frozen encoders included: all ranks must
@@ -120,11 +120,12 @@ class FusionTrainer:
         without autograd). In a single process the two encoders run on two HIP streams — they are
         independent until the head, so one's MFMA main loops overlap the other's HBM-bound
         epilogues, attention and LayerNorms and fill its last-round GEMM tiles; autograd runs each
-        encoder's backward on its forward stream and joins them before the optimizer."""
+        encoder's backward on its forward stream and joins them before the optimizer (the DP
+        all-reduce buckets gradients per stream, mmfd.dp)."""
         ids = batch["input_ids"].to(dev, non_blocking=True)
         mask = batch["attention_mask"].to(dev, non_blocking=True)
         pix = batch["pixel_values"].to(dev, non_blocking=True)
-        conc = self.concurrent and self.dp is None
+        conc = self.concurrent
         main = torch.cuda.current_stream(dev)
         if conc:
             side = self._side_stream(dev)
