@@ -134,18 +134,16 @@ def cpu_baseline(dev, steps=3, batch=4):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (tools/profile.sh ->
-    profiles/<tag>_hbm_traffic.json: FETCH_SIZE x2 + WRITE_SIZE), or None when absent."""
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary that lists it
+    (tools/profile.sh -> profiles/<tag>_hbm_traffic.json: FETCH_SIZE x2 + WRITE_SIZE), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel)
-    if k is None:
-        return None, os.path.basename(files[-1])
-    return int(k["traffic_bytes_per_dispatch"]), os.path.basename(files[-1])
+    for path in reversed(files):
+        with open(path) as f:
+            k = json.load(f).get("kernels", {}).get(kernel)
+        if k is not None:
+            return int(k["traffic_bytes_per_dispatch"]), os.path.basename(path)
+    return None, (os.path.basename(files[-1]) if files else None)
 
 
 def extract_main(args, dev, world, rank):
