@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(NT, 1)
 gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
                float alpha, int tiles_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
-               int rs_mode) {
+               int rs_mode, int group_m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -561,7 +561,16 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   G8_STAMP(0);
   const int gx = gridDim.x, gy = gridDim.y;
   const int tile = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
-  const int64_t m0 = (int64_t)(tile / gx) * G8_BM, n0 = (int64_t)(tile % gx) * G8_BN;
+  // grouped raster: an XCD's consecutive tiles sweep group_m row panels x the column tiles, so the
+  // ~32 tiles it runs at once share group_m A panels and 32/group_m B panels in its L2
+  int trow, tcol;
+  {
+    const int gsz = group_m * gx, g = tile / gsz, first = g * group_m, gm = min(gy - first, group_m);
+    const int r = tile - g * gsz;
+    trow = first + r % gm;
+    tcol = r / gm;
+  }
+  const int64_t m0 = (int64_t)trow * G8_BM, n0 = (int64_t)tcol * G8_BN;
   constexpr int G8_BK = G8T<T>::BK;
   constexpr int64_t ESZ = sizeof(T);
   const int nkt_total = (int)((K + G8_BK - 1) / G8_BK);
@@ -627,7 +636,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 
   // fused row sums of op(A) (bias gradient): blocks of the first column tile only; wave wc sums
   // A subtile i == wc of each A fragment set it loads, lane (g, i) covering k-chunk g of row i
-  const bool do_rs = rs_mode != 0 && (tile % gx) == 0;
+  const bool do_rs = rs_mode != 0 && tcol == 0;
   float rs0 = 0.f, rs1 = 0.f;
 
   uint4 fa[4][2], fb[2][2];
@@ -1042,6 +1051,11 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
                      a.alpha, tps, e);
 }
 
+int g8_group_m() {
+  static const int gm = getenv("MMFD_G8_GROUP_M") ? std::max(1, atoi(getenv("MMFD_G8_GROUP_M"))) : 1;
+  return gm;
+}
+
 template <typename T, int TA, int TB, typename TC, bool PRE>
 void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
                  int rs_mode, hipStream_t s) {
@@ -1053,7 +1067,7 @@ void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
   (void)attr;
   hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE>), grid, dim3(NT), G8_LDS, s, (const T*)a.A, a.lda,
                      (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
-                     a.a_rowsum_beta, rs_mode);
+                     a.a_rowsum_beta, rs_mode, g8_group_m());
 }
 
 template <typename T, int TA, int TB, typename TC>
