@@ -17,6 +17,7 @@
 // Dropout on P (layers.py:53 / SDPA dropout_p) is counter based: index ((b*H+h)*Lq+q)*Lk+k.
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 #include <math.h>
 #include <stdlib.h>
 
@@ -643,14 +644,18 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
     f32x4 o[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < lk_pad; k0 += 64) {
-      const int nsub = min(4, (lk_pad - k0) >> 4);  // 16-key subtiles present in this chunk
+    // one 64-key chunk with NS 16-key subtiles present (NS < 4 only for the last, padded chunk;
+    // NS = 0: that count at run time, `ns_rt`); a compile-time NS keeps every per-subtile branch
+    // out of the full chunks
+    auto chunk = [&](int k0, auto nsc, int ns_rt) {
+      constexpr int NS = decltype(nsc)::value;
+      const int nsub = NS ? NS : ns_rt;
       const char* kc_img = k_img + k0 * C::RB;
       const char* vc_img = v_img + k0 * C::RB;
       f32x4 s[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (nsub == 4) {  // full chunk: four interleaved S^T chains, K fragments read one k-chunk ahead
+      if (sizeof(T) == 4 && nsub == 4) {  // fp32: four interleaved S^T chains, K read one k-chunk ahead
         uint4 fa[4], fb[4], fn[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) { fa[ks] = row_frag<T, D>(kc_img, ks, 0, lane); fb[ks] = qf[0]; }
@@ -668,7 +673,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
         }
       } else {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
+        for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
           if (ks < nsub) {
 #pragma unroll
             for (int kc = 0; kc < C::KCH; ++kc) Mma<T>::run(s[ks], row_frag<T, D>(kc_img, ks, kc, lane), qf[kc]);
@@ -677,11 +682,8 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (ks >= nsub) {
-          s[ks] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-          continue;
-        }
+      for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
+        if (ks >= nsub) continue;
         const float4 kb4 = *reinterpret_cast<const float4*>(kbias + k0 + ks * 16 + 4 * g);
         const float kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
         float rb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -711,7 +713,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float rs = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
         if (ks >= nsub) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -734,7 +736,7 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
         for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
       }
 #pragma unroll
-      for (int c = 0; c < 4 / SUBS; ++c) {
+      for (int c = 0; c < (NS ? NS : 4) / SUBS; ++c) {
         if (c * SUBS >= nsub) continue;
         uint4 fa[C::DT], fb[C::DT];
         const uint4 a = pack_acc<T>(s, c);
@@ -742,6 +744,17 @@ __global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
         for (int d = 0; d < C::DT; ++d) { fa[d] = a; fb[d] = tr_frag<T, D>(vc_img, c, d, lane); }
         Mma<T>::template runN<C::DT>(o, fa, fb);
       }
+    };
+    if constexpr (SUBS == 1) {
+      // fp32 (MFMA-bound): one instance with the subtile count at run time — two compile-time
+      // instances (full chunk + tail) raised it from 154 to 255 VGPRs and cost 7 % at L = 128
+      for (int k0 = 0; k0 < lk_pad; k0 += 64) chunk(k0, std::integral_constant<int, 0>{}, min(4, (lk_pad - k0) >> 4));
+    } else {
+      // bf16 (VALU-bound): the full chunks free of per-subtile branches (128 VGPRs: two workgroups
+      // per CU), the 32-key padded tail as its own instance
+      int k0 = 0;
+      for (; k0 + 64 <= lk_pad; k0 += 64) chunk(k0, std::integral_constant<int, 4>{}, 4);
+      if (k0 < lk_pad) chunk(k0, std::integral_constant<int, 2>{}, 2);
     }
     lsum += __shfl_xor(lsum, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
@@ -939,17 +952,25 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // K / V row fragments of the first key chunk; each iteration prefetches the next chunk's
+    // fp32 (MFMA-bound, two waves per SIMD whatever the registers): K / V row fragments of the
+    // next key chunk and this chunk's transposed K are read ahead; bf16 reads them where they are
+    // used, which keeps the kernel at <= 128 VGPRs and two workgroups per CU (the read-ahead form
+    // measured 211 -> 298 us per ViT/BERT call in bf16)
+    constexpr bool PF = sizeof(T) == 4;
     uint4 ka[SUBS * C::KCH], va[SUBS * C::KCH];
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < SUBS * C::KCH; ++i) {
-      ka[i] = row_frag<T, D>(k_row, i / C::KCH, i % C::KCH, lane);
-      va[i] = row_frag<T, D>(v_row, i / C::KCH, i % C::KCH, lane);
+      for (int i = 0; i < SUBS * C::KCH; ++i) {
+        ka[i] = row_frag<T, D>(k_row, i / C::KCH, i % C::KCH, lane);
+        va[i] = row_frag<T, D>(v_row, i / C::KCH, i % C::KCH, lane);
+      }
     }
     for (int kc2 = 0; kc2 < nkc; ++kc2) {
-      uint4 tk[C::DT];  // transposed K fragments (B operand of dQ), read ahead of the softmax
+      uint4 tk[C::DT];  // transposed K fragments (B operand of dQ)
+      if constexpr (PF) {
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) tk[d] = tr_frag<T, D>(k_tr, kc2, d, lane);
+        for (int d = 0; d < C::DT; ++d) tk[d] = tr_frag<T, D>(k_tr, kc2, d, lane);
+      }
       f32x4 sd[2 * SUBS];
 #pragma unroll
       for (int i = 0; i < 2 * SUBS; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -958,12 +979,19 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
         uint4 fa[2 * SUBS], fb[2 * SUBS];
 #pragma unroll
         for (int h2 = 0; h2 < SUBS; ++h2) {
-          fa[2 * h2] = ka[h2 * C::KCH + kc]; fb[2 * h2] = qf[kc];
-          fa[2 * h2 + 1] = va[h2 * C::KCH + kc]; fb[2 * h2 + 1] = dof[kc];
+          if constexpr (PF) {
+            fa[2 * h2] = ka[h2 * C::KCH + kc];
+            fa[2 * h2 + 1] = va[h2 * C::KCH + kc];
+          } else {
+            fa[2 * h2] = row_frag<T, D>(k_row, SUBS * kc2 + h2, kc, lane);
+            fa[2 * h2 + 1] = row_frag<T, D>(v_row, SUBS * kc2 + h2, kc, lane);
+          }
+          fb[2 * h2] = qf[kc];
+          fb[2 * h2 + 1] = dof[kc];
         }
         Mma<T>::template runN<2 * SUBS>(sd, fa, fb);
       }
-      if (kc2 + 1 < nkc) {
+      if (PF && kc2 + 1 < nkc) {
 #pragma unroll
         for (int i = 0; i < SUBS * C::KCH; ++i) {
           ka[i] = row_frag<T, D>(k_row, SUBS * (kc2 + 1) + i / C::KCH, i % C::KCH, lane);
@@ -994,7 +1022,10 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
       const uint4 as = pack_acc<T>(ds, 0);
       uint4 fa[C::DT];
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) fa[d] = as;
+      for (int d = 0; d < C::DT; ++d) {
+        fa[d] = as;
+        if constexpr (!PF) tk[d] = tr_frag<T, D>(k_tr, kc2, d, lane);
+      }
       Mma<T>::template runN<C::DT>(dq, fa, tk);
     }
 #pragma unroll
