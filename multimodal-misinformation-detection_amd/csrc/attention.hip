@@ -583,8 +583,11 @@ __device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t 
     dst[i] = i < p.Lk ? (p.key_bias ? fmaxf(p.key_bias[b * p.Lk + i] * LOG2E, -1e30f) : 0.f) : -INFINITY;
 }
 
+// bf16 without the relative bias: at most 128 VGPRs (4 waves per SIMD) so that two 8-wave
+// workgroups share a CU — the bf16 K/V images allow it, and one VGPR over halves the occupancy
+// (ViT fwd +45 %); the REL instantiation needs ~148 and would spill under that bound
 template <typename T, int D, int HPB, bool REL>
-__global__ void __launch_bounds__(V2_THREADS) attn_fwd_v2_kernel(AttnP p) {
+__global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) attn_fwd_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
   // domain) over 64-key chunks (the last one holds only the padded key count's subtiles); key
   // mask/padding come from a per-key bias vector in LDS.
@@ -869,19 +872,21 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
         const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qs * 16 + 4 * g);
         const float4 d4 = *reinterpret_cast<const float4*>(s_delta + qs * 16 + 4 * g);
         const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+        float z[4] = {1.f, 1.f, 1.f, 1.f};
+        if (p.p > 0.f) {  // one uniform branch per subtile; the element index advances by Lk per query
+          uint64_t idx = hcol + (uint64_t)(qs * 16 + 4 * g) * (uint64_t)p.Lk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r, idx += (uint64_t)p.Lk)
+            z[r] = (mmfd_hash_k(hkey, idx) < p.thr) ? 0.f : p.keep_scale;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int lq = qs * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kb2);
           if (REL && lq < p.Lq && mykey < p.Lk) t = fmaf(relcol[(int64_t)lq * p.Lk], LOG2E, t);
           const float pr = __builtin_amdgcn_exp2f(t - lq2[r]);
-          float z = 1.f;
-          if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, hcol + (uint64_t)lq * (uint64_t)p.Lk);
-            z = (hsh < p.thr) ? 0.f : p.keep_scale;
-          }
-          pd[h2][r] = pr * z;
-          ds[h2][r] = pr * (dp[r] * z - dl[r]);
+          pd[h2][r] = pr * z[r];
+          ds[h2][r] = pr * (dp[r] * z[r] - dl[r]);
         }
       }
       const uint4 ap = pack_acc<T>(pd, 0);
@@ -911,7 +916,7 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
 }
 
 template <typename T, int D, bool REL>
-__global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
+__global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2_kernel(AttnP p) {
   // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K (REL as in dK/dV)
   using C = AT<T, D>;
   constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
@@ -1005,18 +1010,19 @@ __global__ void __launch_bounds__(V2_THREADS) attn_dq_v2_kernel(AttnP p) {
         const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
         const float4 kb4 = *reinterpret_cast<const float4*>(kbias + ks * 16 + 4 * g);
         const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
+        float z[4] = {1.f, 1.f, 1.f, 1.f};
+        if (p.p > 0.f) {  // one uniform branch per subtile
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            z[r] = (mmfd_hash_k(hkey, hrow + (uint64_t)(ks * 16 + 4 * g + r)) < p.thr) ? 0.f : p.keep_scale;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = ks * 16 + 4 * g + r;
           float t = fmaf(sv[r], c2, kbr[r]);
           if (REL && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
           const float pr = __builtin_amdgcn_exp2f(t - lse2);
-          float z = 1.f;
-          if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)key);
-            z = (hsh < p.thr) ? 0.f : p.keep_scale;
-          }
-          ds[h2][r] = pr * (dp[r] * z - dlt);
+          ds[h2][r] = pr * (dp[r] * z[r] - dlt);
         }
       }
       const uint4 as = pack_acc<T>(ds, 0);
