@@ -721,12 +721,15 @@ def train_leg(args, dev, world, rank, precision):
     ms = 1000.0 * elapsed / args.steps
     pairs = args.batch * world * args.steps / elapsed
     loss_val = loss[0].item()
+    log(f"{precision} timed: {pairs:.1f} pairs/s, {ms:.1f} ms/step")
 
     # per-GEMM device times from two more eager steps of the same trainer after the timed region
     # (events cannot be timed inside a graph), with the two encoders on ONE stream: in the timed
     # step they overlap on two streams, which is faster overall but stretches each kernel's
     # duration by the CUs the other stream holds — the roofline is a property of the kernel alone
     steps_in_prof = 2
+    if graphed:  # the graph's private pool would double the eager probe's footprint
+        tr.release_graph()
     conc, tr.concurrent = tr.concurrent, False
     with probe:
         for _ in range(steps_in_prof):
@@ -736,6 +739,16 @@ def train_leg(args, dev, world, rank, precision):
     dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[precision]
+    # split-operand fp32 GEMM (gemm.hip X6): six bf16 MFMA products per fp32 product, so the
+    # hardware roofline is the bf16 MFMA peak over the executed products; the fp32 view (2MNK over
+    # the fp32 MFMA peak) is reported beside it
+    x6 = dom_name.rstrip().endswith("true>")
+    fp32_view = None
+    if x6:
+        fp32_view = {"achieved": round(achieved, 1), "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_TFLOPS["fp32"], 4),
+                     "note": "algorithmic fp32 FLOPs (2MNK) / time vs the fp32 MFMA dense peak"}
+        achieved, peak = 6 * achieved, PEAK_TFLOPS["bf16"]
     gemm_ms = sum(v["ms"] for v in prof.values()) / steps_in_prof
     gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(dom_name)
@@ -754,7 +767,10 @@ def train_leg(args, dev, world, rank, precision):
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "launches_per_step": d["launches"] // steps_in_prof,
                          "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
-                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"])}}
+                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"]) * (6 if x6 else 1),
+                         **({"fp32_equivalent": fp32_view, "flops_note": "bf16 MFMA FLOPs: 6 x 2MNK per launch "
+                             "(products mid*mid, hi*lo, lo*hi, hi*mid, mid*hi, hi*hi of the split operands)"}
+                            if x6 else {})}}
 
 
 def spawn_ranks(n):

@@ -89,12 +89,31 @@ typedef struct mmfd_gemm_args {
      replacing the reference's autograd of nn.Linear.bias): a_rowsum[m] = a_rowsum_beta *
      a_rowsum[m] + sum_k op(A)[m][k], fp32, M entries. NULL disables. */
   float* a_rowsum; float a_rowsum_beta;
+  /* optional bf16 planes [3][rows][cols] of the stored fp32 A / B (mmfd_split3), for the split-
+     operand fp32 GEMM (mmfd_set_fp32_gemm_mode): a product whose operand was already split — the
+     forward input reused by the weight-gradient GEMM, the output gradient shared by the data- and
+     weight-gradient GEMMs — reads them instead of splitting again. NULL = split here. Ignored by
+     the other paths. */
+  const void* a_planes; const void* b_planes;
 } mmfd_gemm_args;
 
 int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);
 /* bytes of workspace the automatic split choice would like for this problem (incl. the per-split
-   row-sum partials when a_rowsum is set) */
+   row-sum partials when a_rowsum is set, and the bf16 operand planes of a split-operand fp32 GEMM) */
 int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* args);
+/* the split-K factor mmfd_gemm picks for these arguments (given the workspace it asked for) */
+int mmfd_gemm_splits(const mmfd_gemm_args* args);
+/* fp32 x fp32 -> fp32 GEMMs (the reference's nn.Linear arithmetic, model.py / layers.py Linears):
+   mode 1 (default; env MMFD_FP32_GEMM=native selects 0 at load) splits each fp32 operand into three
+   bf16 planes x = hi + mid + lo (written to the workspace) and accumulates the six products
+   mid*mid, hi*lo, lo*hi, hi*mid, mid*hi, hi*hi on the bf16 MFMA in fp32 — 24 operand bits, products
+   exact, the accumulation an fp32 sum (error measured at the fp32 MFMA's level, tests/
+   test_kernels_gpu.py); mode 0 = the fp32 MFMA (v_mfma_f32_16x16x4f32). Used only when
+   workspace_bytes covers mmfd_gemm_workspace_bytes. Returns the previous mode. */
+int mmfd_set_fp32_gemm_mode(int mode);
+/* fp32 [rows][ld] -> bf16 planes [3][rows][cols] (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid);
+   cols % 8 == 0, 16-B aligned rows) */
+int mmfd_split3(int64_t rows, int64_t cols, const float* x, int64_t ld, void* planes, mmfd_stream_t stream);
 
 /* Column sums (bias gradients): out[n] = beta*out[n] + sum_m X[m*ldx + n]. workspace >= 4*N*256 B */
 int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, float* out, float beta,

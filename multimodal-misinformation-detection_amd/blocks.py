@@ -212,6 +212,15 @@ class StepCtx:
         self.shadows[("derived", key)] = (sig, t)
         return t
 
+    def planes(self, t):
+        """bf16 planes of an fp32 GEMM operand (kernels.split3) when the fp32 GEMMs run on split
+        operands, else None: split once, read by every GEMM that takes `t` (the forward input
+        again by its weight-gradient GEMM, an output gradient by the data- and weight-gradient
+        GEMMs) instead of being split inside each of them"""
+        if self.dt != torch.float32 or not K.split_eligible(t):
+            return None
+        return K.split3(t)
+
     # ---- dropout -------------------------------------------------------------------------------
     def drop(self, site):
         """(p, seed, salt) kwargs for a dropout site; p=0 when not training."""
@@ -239,17 +248,18 @@ class StepCtx:
             return g, 0.0
         return g, 1.0
 
-    def lin_grads(self, names, dy2d, x2d):
+    def lin_grads(self, names, dy2d, x2d, dyp=None, xp=None):
         if self.side is None:
-            return self._lin_grads(names, dy2d, x2d)
+            return self._lin_grads(names, dy2d, x2d, dyp, xp)
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
-            self._lin_grads(names, dy2d, x2d)
-        dy2d.record_stream(self.side)
-        x2d.record_stream(self.side)
+            self._lin_grads(names, dy2d, x2d, dyp, xp)
+        for t in (dy2d, x2d, dyp, xp):
+            if t is not None:
+                t.record_stream(self.side)
         self._side_used = True
 
-    def _lin_grads(self, names, dy2d, x2d):
+    def _lin_grads(self, names, dy2d, x2d, dyp=None, xp=None):
         """dW = dy^T x (fp32, accumulate) with db = sum_rows(dy) fused into the same GEMM
         (a_rowsum); `names` are the row blocks of dy. A packed group (fused QKV / K|V) whose
         gradients are first written here is ONE GEMM into a packed buffer whose row blocks become
@@ -262,7 +272,7 @@ class StepCtx:
             dev = self.P[names[0] + ".weight"].device
             gw = torch.empty((sum(rows), kin), device=dev, dtype=torch.float32)
             gb = torch.empty(sum(rows), device=dev, dtype=torch.float32)
-            K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=gw, a_rowsum=gb)
+            K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=gw, a_rowsum=gb, a_planes=dyp, b_planes=xp)
             r = 0
             for n, k in zip(names, rows):
                 self.grads[n + ".weight"] = gw[r:r + k]
@@ -274,14 +284,15 @@ class StepCtx:
             g, beta = self.grad_slot(n + ".weight", self.P[n + ".weight"].shape)
             if n + ".bias" in self.P:
                 gb, bb = self.grad_slot(n + ".bias", self.P[n + ".bias"].shape)
-                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta, a_rowsum=gb, a_rowsum_beta=bb)
+                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta, a_rowsum=gb, a_rowsum_beta=bb,
+                       a_planes=dyp, b_planes=xp)
             else:
-                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta)
+                K.gemm(dy2d, x2d, trans_a=True, trans_b=True, out=g, beta=beta, a_planes=dyp, b_planes=xp)
             return
         r = 0
         for n in names:
             rows = self.P[n + ".weight"].shape[0]
-            self._lin_grads([n], dy2d[:, r:r + rows], x2d)
+            self._lin_grads([n], dy2d[:, r:r + rows], x2d, None, xp)
             r += rows
 
 
@@ -293,26 +304,26 @@ def as2d(x):
 # linear
 # -------------------------------------------------------------------------------------------------
 def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=None, drop_site=None,
-           out_dtype=None):
+           out_dtype=None, xp=None):
     W = ctx.w(name)
     aux = None
     if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
         aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
     y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,
-               **(ctx.drop(drop_site) if drop_site else {}))
+               a_planes=xp, **(ctx.drop(drop_site) if drop_site else {}))
     return y, aux
 
 
-def linear_packed(ctx: StepCtx, x2d, names):
+def linear_packed(ctx: StepCtx, x2d, names, xp=None):
     W, b = ctx.w_packed(names)
-    return K.gemm(x2d, W, bias=b)
+    return K.gemm(x2d, W, bias=b, a_planes=xp)
 
 
 def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
-              residual=None):
+              residual=None, dyp=None):
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
     return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
-                  residual=residual, **(ctx.drop(drop_site) if drop_site else {}))
+                  residual=residual, a_planes=dyp, **(ctx.drop(drop_site) if drop_site else {}))
 
 
 # -------------------------------------------------------------------------------------------------

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -548,12 +549,23 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 
 // PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
 // prefetched for all of a thread's rows before the accumulators are staged (see the epilogue)
-template <typename T, int TA, int TB, typename TC, bool PRE>
+// X6 (fp32 GEMMs from bf16 split operands, see mmfd_gemm): A and B are three bf16 planes each
+// (x = hi + mid + lo), x6.pa / x6.pb bytes apart; the K loop runs over six segments of x6.nkt
+// K-tiles, segment s multiplying A plane X6_CA[s] with B plane X6_CB[s]. The segments go from the
+// smallest products to hi*hi, so the fp32 accumulator collects the 2^-16 / 2^-8 correction terms
+// first and then takes the K hi*hi products (exact in fp32) exactly as a plain fp32 sum would: the
+// rounding of the result is that of the fp32 dot product.
+struct X6Args { int nkt; uint32_t pa, pb; };
+constexpr uint32_t X6_CA = 0x121;  // A planes per segment (2 bits each): m h l h m h
+constexpr uint32_t X6_CB = 0x049;  // B planes per segment:                m l h m h h
+constexpr uint32_t X6_RS = 0x25;   // segments whose A plane appears once (m, l, h): row sums of op(A)
+
+template <typename T, int TA, int TB, typename TC, bool PRE, bool X6>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
                float alpha, int tiles_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
-               int rs_mode, int group_m) {
+               int rs_mode, int group_m, X6Args x6) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -573,7 +585,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   const int64_t m0 = (int64_t)trow * G8_BM, n0 = (int64_t)tcol * G8_BN;
   constexpr int G8_BK = G8T<T>::BK;
   constexpr int64_t ESZ = sizeof(T);
-  const int nkt_total = (int)((K + G8_BK - 1) / G8_BK);
+  const int nkt_total = X6 ? 6 * x6.nkt : (int)((K + G8_BK - 1) / G8_BK);
   const int kt0 = blockIdx.z * tiles_per_split;
   const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
 
@@ -587,8 +599,8 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * ESZ);
-  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * ESZ);
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, X6 ? 3 * (int64_t)x6.pa : (TA == 0 ? M : K) * lda * ESZ);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, X6 ? 3 * (int64_t)x6.pb : (TB == 0 ? N : K) * ldb * ESZ);
   Fill<T, TA, 128, 2> fa0, fa1;
   Fill<T, TB, 128, 2, 1> fb0, fb1;
   fa0.init(lda, m0, M, wave, lane);
@@ -599,14 +611,20 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   // half-tile h of K-tile t: 0 = A-h0, 1 = A-h1, 2 = B-h0, 3 = B-h1; buffer t & 1
   auto img = [&](int t, int h) -> char* { return smem + ((t & 1) * 4 + h) * G8_HALF; };
   auto issue = [&](int h, int t) {
-    const int64_t k0 = (int64_t)(kt0 + t) * G8_BK;
+    int64_t k0 = (int64_t)(kt0 + t) * G8_BK;
+    uint32_t pofs = 0;  // X6: byte offset of the segment's plane
+    if constexpr (X6) {
+      const int v = kt0 + t, sg = v / x6.nkt;
+      k0 = (int64_t)(v - sg * x6.nkt) * G8_BK;
+      pofs = h < 2 ? ((X6_CA >> (2 * sg)) & 3u) * x6.pa : ((X6_CB >> (2 * sg)) & 3u) * x6.pb;
+    }
     const bool tail = k0 + G8_BK > K;
     if (h < 2) {
-      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * ESZ);
+      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * ESZ) + pofs;
       if (h == 0) fa0.issue(rsa, img(t, 0), so, tail, k0, K, wave, lane);
       else fa1.issue(rsa, img(t, 1), so, tail, k0, K, wave, lane);
     } else {
-      const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * ESZ);
+      const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * ESZ) + pofs;
       if (h == 2) fb0.issue(rsb, img(t, 2), so, tail, k0, K, wave, lane);
       else fb1.issue(rsb, img(t, 3), so, tail, k0, K, wave, lane);
     }
@@ -638,6 +656,8 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   // A subtile i == wc of each A fragment set it loads, lane (g, i) covering k-chunk g of row i
   const bool do_rs = rs_mode != 0 && tcol == 0;
   float rs0 = 0.f, rs1 = 0.f;
+  // X6: only the segments that carry each A plane once contribute to the row sums
+  auto rs_on = [&](int t) { return !X6 || ((X6_RS >> ((kt0 + t) / x6.nkt)) & 1u); };
 
   uint4 fa[4][2], fb[2][2];
   if constexpr (PH2) {
@@ -653,7 +673,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
       g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
       g8_frag_b<T, TB>(fbh, img(t, 3), wc, lane);
-      if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (do_rs && rs_on(t)) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
       if (t + 1 < nk) {
         issue(1, t + 1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -665,7 +685,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_barrier();
       // phase Y(t)
       g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
-      if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (do_rs && rs_on(t)) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
       if (t + 2 < nk) {
         issue(0, t + 2); issue(2, t + 2); issue(3, t + 2);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -1056,39 +1076,89 @@ int g8_group_m() {
   return gm;
 }
 
-template <typename T, int TA, int TB, typename TC, bool PRE>
+template <typename T, int TA, int TB, typename TC, bool PRE, bool X6>
 void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
-                 int rs_mode, hipStream_t s) {
+                 int rs_mode, hipStream_t s, const void* A, int64_t lda, const void* B, int64_t ldb, X6Args x6) {
   dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<T, TA, TB, TC, PRE>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<T, TA, TB, TC, PRE, X6>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE>), grid, dim3(NT), G8_LDS, s, (const T*)a.A, a.lda,
-                     (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
-                     a.a_rowsum_beta, rs_mode, g8_group_m());
+  hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE, X6>), grid, dim3(NT), G8_LDS, s, (const T*)A, lda,
+                     (const T*)B, ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
+                     a.a_rowsum_beta, rs_mode, g8_group_m(), x6);
 }
 
 template <typename T, int TA, int TB, typename TC>
 void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
-               int rs_mode, hipStream_t s) {
+               int rs_mode, hipStream_t s, const X6Args* x6, const void* xa, const void* xb) {
+  if constexpr (std::is_same<T, bf16>::value && std::is_same<TC, float>::value) {
+    if (x6) {  // split-operand fp32 GEMM: A / B are the bf16 planes, leading dim = stored columns
+      const int64_t lda = TA == 0 ? a.K : a.M, ldb = TB == 0 ? a.K : a.N;
+      return launch_g8_v<T, TA, TB, TC, false, true>(a, e, ws, splits, tps, rs_out, rs_mode, s, xa, lda, xb, ldb, *x6);
+    }
+  }
   const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
   const int streams = (e.residual ? 1 : 0) + (bwd_act ? 1 : 0) + (e.beta != 0.f ? 1 : 0);
+  const X6Args none{1, 0, 0};
   if constexpr (std::is_same<TC, bf16>::value) {
-    if (streams == 1 && !ws && e.vec) return launch_g8_v<T, TA, TB, TC, true>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+    if (streams == 1 && !ws && e.vec)
+      return launch_g8_v<T, TA, TB, TC, true, false>(a, e, ws, splits, tps, rs_out, rs_mode, s, a.A, a.lda, a.B, a.ldb, none);
   }
-  launch_g8_v<T, TA, TB, TC, false>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+  launch_g8_v<T, TA, TB, TC, false, false>(a, e, ws, splits, tps, rs_out, rs_mode, s, a.A, a.lda, a.B, a.ldb, none);
 }
 
 template <typename T, typename TC>
 void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
-                 int rs_mode, hipStream_t s) {
-  if (!a.trans_a && !a.trans_b) launch_g8<T, 0, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else if (!a.trans_a && a.trans_b) launch_g8<T, 0, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else if (a.trans_a && !a.trans_b) launch_g8<T, 1, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
-  else launch_g8<T, 1, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s);
+                 int rs_mode, hipStream_t s, const X6Args* x6 = nullptr, const void* xa = nullptr,
+                 const void* xb = nullptr) {
+  if (!a.trans_a && !a.trans_b) launch_g8<T, 0, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s, x6, xa, xb);
+  else if (!a.trans_a && a.trans_b) launch_g8<T, 0, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s, x6, xa, xb);
+  else if (a.trans_a && !a.trans_b) launch_g8<T, 1, 0, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s, x6, xa, xb);
+  else launch_g8<T, 1, 1, TC>(a, e, ws, splits, tps, rs_out, rs_mode, s, x6, xa, xb);
 }
+
+// fp32 operand -> three bf16 planes (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid),
+// each difference exact in fp32): stored rows x cols (ld) -> planes [3][rows][cols]; 8 columns per
+// thread (two 16-B loads, one 16-B store per plane), cols % 8 == 0
+__global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ X, int64_t ldx, int64_t rows,
+                                                     int64_t cols, bf16* __restrict__ P, int64_t plane) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= cols) return;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const float4 x0 = *reinterpret_cast<const float4*>(X + r * ldx + c);
+    const float4 x1 = *reinterpret_cast<const float4*>(X + r * ldx + c + 4);
+    const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    bf16x8 h, m, l;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bf16 hu = (bf16)x[u];
+      const float r1 = x[u] - (float)hu;
+      const bf16 mu = (bf16)r1;
+      h[u] = hu;
+      m[u] = mu;
+      l[u] = (bf16)(r1 - (float)mu);
+    }
+    bf16* d = P + r * cols + c;
+    *reinterpret_cast<uint4*>(d) = __builtin_bit_cast(uint4, h);
+    *reinterpret_cast<uint4*>(d + plane) = __builtin_bit_cast(uint4, m);
+    *reinterpret_cast<uint4*>(d + 2 * plane) = __builtin_bit_cast(uint4, l);
+  }
+}
+
+void launch_split3(const float* X, int64_t ldx, int64_t rows, int64_t cols, bf16* P, hipStream_t s) {
+  const unsigned gx = (unsigned)((cols + 2047) / 2048);
+  const unsigned gy = (unsigned)std::min<int64_t>(rows, std::max<int64_t>(1, 16384 / gx));
+  hipLaunchKernelGGL(split3_kernel, dim3(gx, gy), dim3(256), 0, s, X, ldx, rows, cols, P, rows * cols);
+}
+
+// fp32 x fp32 -> fp32 GEMM mode: 1 = split operands (six bf16 MFMA products per fp32 product, see
+// gemm256_kernel's X6 note; about 1.6x the fp32 MFMA rate at the encoder shapes), 0 = fp32 MFMA
+int g_fp32_mode = [] {
+  const char* v = getenv("MMFD_FP32_GEMM");
+  return (v && (!strcmp(v, "native") || !strcmp(v, "0"))) ? 0 : 1;
+}();
 
 bool use_g8(const mmfd_gemm_args& a) {
   static const bool off = getenv("MMFD_GEMM_V1") != nullptr;
@@ -1129,9 +1199,9 @@ bool mfma_ok(const mmfd_gemm_args& a) {
   return true;
 }
 
-int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
-  const int T = (a.dtype == MMFD_BF16) ? 64 : 32;
-  const int64_t nkt = (a.K + T - 1) / T;
+int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed, bool x6 = false) {
+  const int T = (a.dtype == MMFD_BF16 || x6) ? 64 : 32;
+  const int64_t nkt = x6 ? 6 * ((a.K + 63) / 64) : (a.K + T - 1) / T;
   int splits = 1;
   if (use_g8(a)) {
     // one 256x256 block per CU: pick the split count that minimises rounds-of-256 per unit of work
@@ -1142,7 +1212,7 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
       // overhead) + the fp32 slab round trip (written by the blocks, read by the reduce) at ~5 TB/s
       double best = 1e30;
       const int smax = (int)std::min<int64_t>(32, nkt / 8);
-      const double kt_us = a.dtype == MMFD_BF16 ? 1.8 : 7.0;  // one 256x256 K-tile (bf16 / fp32 MFMA rate)
+      const double kt_us = (a.dtype == MMFD_BF16 || x6) ? 1.8 : 7.0;  // one 256x256 K-tile (bf16 / fp32 MFMA rate)
       for (int sp = 1; sp <= smax; ++sp) {
         const double rounds = (double)((tiles * sp + 255) / 256);
         const double kts = (double)((nkt + sp - 1) / sp);
@@ -1164,6 +1234,26 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed) {
   *ws_bytes_needed = (splits > 1) ? (int64_t)splits * a.M * a.N * 4 : 0;
   return splits;
 }
+
+
+// split-operand eligibility: fp32 in / fp32 out on the 256x256 path, stored column counts a
+// multiple of 8 (16-B plane rows), three planes of each operand < 2 GB (32-bit buffer offsets), and
+// K a whole number of 64-row tiles when an operand is MN-contiguous (its K rows are plane rows:
+// a partial tile would read into the next plane)
+struct X6Plan { bool on; int64_t rows_a, cols_a, rows_b, cols_b, pa, pb; };
+X6Plan x6_plan(const mmfd_gemm_args& a) {
+  X6Plan p{};
+  if (g_fp32_mode != 1 || a.dtype != MMFD_F32 || a.c_dtype != MMFD_F32 || !use_g8(a)) return p;
+  p.rows_a = a.trans_a ? a.K : a.M; p.cols_a = a.trans_a ? a.M : a.K;
+  p.rows_b = a.trans_b ? a.K : a.N; p.cols_b = a.trans_b ? a.N : a.K;
+  if (p.cols_a % 8 || p.cols_b % 8) return p;
+  if ((a.trans_a || a.trans_b) && a.K % 64) return p;
+  p.pa = p.rows_a * p.cols_a * 2; p.pb = p.rows_b * p.cols_b * 2;
+  if (3 * p.pa >= (1ll << 31) - 4096 || 3 * p.pb >= (1ll << 31) - 4096) return p;
+  p.on = true;
+  return p;
+}
+int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 // extra workspace for the fused row sums: per-split partials (G8) or the colsum partials (others)
 int64_t rowsum_ws_bytes(const mmfd_gemm_args& a, int splits, bool g8) {
@@ -1193,9 +1283,26 @@ extern "C" int mmfd_debug_g8_stamps(void* host_dst, int64_t bytes) {
 extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
   if (!a) return 0;
   if (!mfma_ok(*a)) return rowsum_ws_bytes(*a, 1, false);
+  const X6Plan xp = x6_plan(*a);
   int64_t need = 0;
-  const int splits = choose_splits(*a, &need);
-  return need + rowsum_ws_bytes(*a, splits, use_g8(*a));
+  const int splits = choose_splits(*a, &need, xp.on);
+  need += rowsum_ws_bytes(*a, splits, use_g8(*a));
+  if (xp.on)  // + the bf16 planes of the operands not handed over already split
+    need = align256(need) + (a->a_planes ? 0 : align256(3 * xp.pa)) + (a->b_planes ? 0 : 3 * xp.pb);
+  return need;
+}
+
+extern "C" int mmfd_gemm_splits(const mmfd_gemm_args* a) {
+  if (!a || !mfma_ok(*a)) return 1;
+  int64_t need = 0;
+  return choose_splits(*a, &need, x6_plan(*a).on);
+}
+
+extern "C" int mmfd_set_fp32_gemm_mode(int mode) {
+  MMFD_CHECK_ARG(mode == 0 || mode == 1, "mmfd_set_fp32_gemm_mode: mode %d (0 = fp32 MFMA, 1 = split operands)", mode);
+  const int old = g_fp32_mode;
+  g_fp32_mode = mode;
+  return old;
 }
 
 extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
@@ -1245,16 +1352,19 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     return rowsum_fallback(a, a.workspace, a.workspace_bytes, s);
   }
 
+  // split-operand fp32 GEMM only with the full workspace it asked for (else the fp32 MFMA path)
+  X6Plan xp = x6_plan(a);
+  if (xp.on && (a.workspace == nullptr || a.workspace_bytes < mmfd_gemm_workspace_bytes(&a))) xp.on = false;
   int64_t need = 0;
-  int splits = choose_splits(a, &need);
-  if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need + rowsum_ws_bytes(a, splits, use_g8(a)))) {
+  int splits = choose_splits(a, &need, xp.on);
+  if (!xp.on && splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need + rowsum_ws_bytes(a, splits, use_g8(a)))) {
     // shrink to what the workspace allows
     const int64_t per = a.M * a.N * 4 + (a.a_rowsum ? a.M * 4 : 0);
     int fit = (a.workspace && per > 0) ? (int)std::min<int64_t>(a.workspace_bytes / per, 32) : 1;
     splits = fit > 1 ? std::min(splits, fit) : 1;
   }
-  const int T = bf ? 64 : 32;
-  const int nkt = (int)((a.K + T - 1) / T);
+  const int T = (bf || xp.on) ? 64 : 32;
+  const int nkt = (int)(xp.on ? 6 * ((a.K + 63) / 64) : (a.K + T - 1) / T);
   const int tps = (nkt + splits - 1) / std::max(splits, 1);
   splits = tps > 0 ? (nkt + tps - 1) / tps : 1;
   if (splits < 1) splits = 1;
@@ -1265,7 +1375,24 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   const int rs_mode = (!a.a_rowsum || !g8) ? 0 : (splits > 1 ? 2 : 1);
   float* rs_out = rs_mode == 2 ? rs_part : a.a_rowsum;
 
-  if (g8 && bf) { if (cbf) dispatch_g8<bf16, bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
+  if (xp.on) {
+    char* planes = (char*)a.workspace + align256((int64_t)(splits > 1 ? splits : 0) * a.M * a.N * 4 +
+                                                 rowsum_ws_bytes(a, splits, true));
+    const bf16* pa = (const bf16*)a.a_planes;
+    const bf16* pb = (const bf16*)a.b_planes;
+    if (!pa) {
+      launch_split3((const float*)a.A, a.lda, xp.rows_a, xp.cols_a, (bf16*)planes, s);
+      pa = (const bf16*)planes;
+      planes += align256(3 * xp.pa);
+    }
+    if (!pb) {
+      launch_split3((const float*)a.B, a.ldb, xp.rows_b, xp.cols_b, (bf16*)planes, s);
+      pb = (const bf16*)planes;
+    }
+    MMFD_CHECK_LAUNCH("split3");
+    const X6Args x6{(int)((a.K + 63) / 64), (uint32_t)xp.pa, (uint32_t)xp.pb};
+    dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s, &x6, pa, pb);
+  } else if (g8 && bf) { if (cbf) dispatch_g8<bf16, bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
   else if (g8) dispatch_g8<float, float>(a, e, ws, splits, tps, rs_out, rs_mode, s);
   else if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }
   else { if (cbf) dispatch_layout<float, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<float, float>(a, e, ws, splits, tps, s); }
@@ -1286,6 +1413,16 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     const int64_t left = a.workspace_bytes - (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
     return rowsum_fallback(a, base, left, s);
   }
+  return 0;
+}
+
+extern "C" int mmfd_split3(int64_t rows, int64_t cols, const float* x, int64_t ld, void* planes, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(rows >= 0 && cols >= 0 && ld >= cols, "mmfd_split3: bad shape");
+  MMFD_CHECK_ARG(cols % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)planes & 15) == 0,
+                 "mmfd_split3: cols must be a multiple of 8 and rows 16-B aligned");
+  if (rows == 0 || cols == 0) return 0;
+  launch_split3(x, ld, rows, cols, (bf16*)planes, (hipStream_t)stream);
+  MMFD_CHECK_LAUNCH("split3");
   return 0;
 }
 

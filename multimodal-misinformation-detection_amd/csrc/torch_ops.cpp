@@ -52,7 +52,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
           double beta, const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& residual,
           bool residual_first, int64_t act, const std::optional<at::Tensor>& aux, double dropout_p,
           const std::optional<at::Tensor>& seed, int64_t salt, int64_t splits, const std::optional<at::Tensor>& a_rowsum,
-          double a_rowsum_beta) {
+          double a_rowsum_beta, const std::optional<at::Tensor>& a_planes = std::nullopt,
+          const std::optional<at::Tensor>& b_planes = std::nullopt) {
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "mmfd::gemm operands must share a dtype");
   mmfd_gemm_args a{};
   a.dtype = dtype_code(A);
@@ -80,6 +81,15 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
   a.splits = (int)splits;
   a.a_rowsum = ptr_or_null<float>(a_rowsum);
   a.a_rowsum_beta = (float)a_rowsum_beta;
+  auto planes = [&](const std::optional<at::Tensor>& p, const at::Tensor& src, const char* name) -> const void* {
+    if (!p.has_value() || !p->defined()) return nullptr;
+    TORCH_CHECK(p->scalar_type() == at::kBFloat16 && p->is_contiguous() && p->dim() == 3 && p->size(0) == 3 &&
+                    p->size(1) == src.size(0) && p->size(2) == src.size(1),
+                "mmfd::gemm: ", name, " must be contiguous bf16 [3, ", src.size(0), ", ", src.size(1), "]");
+    return p->data_ptr();
+  };
+  a.a_planes = planes(a_planes, A, "a_planes");
+  a.b_planes = planes(b_planes, B, "b_planes");
   const int64_t need = mmfd_gemm_workspace_bytes(&a);
   at::Tensor ws;
   if (need > 0) {
@@ -87,6 +97,16 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
     a.workspace = ws.data_ptr(); a.workspace_bytes = need;
   }
   check(mmfd_gemm(&a, stream_of(A)), "mmfd::gemm");
+}
+
+// fp32 [rows, cols] (row-major view) -> bf16 planes [3, rows, cols] (mmfd_split3)
+void split3(const at::Tensor& x, at::Tensor& planes) {
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "mmfd::split3: x must be fp32");
+  TORCH_CHECK(planes.scalar_type() == at::kBFloat16 && planes.is_contiguous() && planes.dim() == 3 &&
+                  planes.size(0) == 3 && planes.size(1) == x.size(0) && planes.size(2) == x.size(1),
+              "mmfd::split3: planes must be contiguous bf16 [3, rows, cols]");
+  check(mmfd_split3(x.size(0), x.size(1), x.data_ptr<float>(), ld2(x, "x"), planes.data_ptr(), stream_of(x)),
+        "mmfd::split3");
 }
 
 // functional nn.Linear forward (x [..., K] @ w[N, K]^T + b, optional fused GELU / ReLU / tanh /
@@ -251,7 +271,8 @@ void topk(const at::Tensor& scores, int64_t k, at::Tensor& values, at::Tensor& i
 TORCH_LIBRARY(mmfd, m) {
   m.def("gemm(Tensor A, Tensor B, bool trans_a, bool trans_b, Tensor(a!) out, float alpha, float beta, Tensor? bias, "
         "Tensor? residual, bool residual_first, int act, Tensor(b!)? aux, float dropout_p, Tensor? seed, int salt, "
-        "int splits, Tensor(c!)? a_rowsum, float a_rowsum_beta) -> ()");
+        "int splits, Tensor(c!)? a_rowsum, float a_rowsum_beta, Tensor? a_planes=None, Tensor? b_planes=None) -> ()");
+  m.def("split3(Tensor x, Tensor(a!) planes) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, int act=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) out, Tensor(b!) lse, int heads, float scale, "
         "Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, float dropout_p, Tensor? seed, int salt, "
@@ -277,6 +298,7 @@ TORCH_LIBRARY(mmfd, m) {
 
 TORCH_LIBRARY_IMPL(mmfd, CUDA, m) {
   m.impl("gemm", &gemm);
+  m.impl("split3", &split3);
   m.impl("linear", &linear);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);

@@ -146,18 +146,25 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
     for i in range(cfg.num_hidden_layers):
         p = f"encoder.layer.{i}"
         s = f"{site}.L{i}"
+        # split-operand fp32 GEMMs: every Linear input is split once here and the planes are kept
+        # for its weight-gradient GEMM (None in bf16 / fp32-MFMA mode)
+        xp = ctx.planes(x) if keep else None
         qkv = Bk.linear_packed(ctx, x, [p + ".attention.self.query", p + ".attention.self.key",
-                                        p + ".attention.self.value"]).view(B, L, 3 * D)
+                                        p + ".attention.self.value"], xp=xp).view(B, L, 3 * D)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         attn_drop = dict(ctx.drop(s + ".attn")) if cfg.attention_probs_dropout_prob > 0 else {}
         o, lse = K.attn_fwd(q, k, v, H, key_bias=kb, **attn_drop)
-        s1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, drop_site=s + ".attn_out")
+        op = ctx.planes(Bk.as2d(o)) if keep else None
+        s1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, drop_site=s + ".attn_out",
+                          xp=op)
         h1, m1, r1 = Bk.layernorm(ctx, s1, p + ".attention.output.LayerNorm", eps)
-        f, pre = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep)
-        s2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=h1, drop_site=s + ".ffn_out")
+        h1p = ctx.planes(h1) if keep else None
+        f, pre = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h1p)
+        fp = ctx.planes(f) if keep else None
+        s2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=h1, drop_site=s + ".ffn_out", xp=fp)
         x_out, m2, r2 = Bk.layernorm(ctx, s2, p + ".output.LayerNorm", eps)
         if keep:
-            states.append((x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop))
+            states.append((x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop, (xp, op, h1p, fp)))
         x = x_out
     st = dict(s0=s0, m0=m0, r0=r0, kb=kb, layers=states, emb_drop=emb_drop) if keep else None
     return x.view(B, L, D), st
@@ -170,27 +177,31 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
     for i in reversed(range(cfg.num_hidden_layers)):
         p = f"encoder.layer.{i}"
         s = f"{site}.L{i}"
-        x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop = st["layers"][i]
+        x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop, (xp, op, h1p, fp) = st["layers"][i]
         ds2, ds2d = Bk.layernorm_bwd(ctx, dx, s2, p + ".output.LayerNorm", m2, r2, drop_site=s + ".ffn_out")
         g2 = ds2d if ds2d is not None else ds2
-        ctx.lin_grads([p + ".output.dense"], g2, f)
-        dpre = Bk.linear_dx(ctx, g2, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre)
-        ctx.lin_grads([p + ".intermediate.dense"], dpre, h1)
+        g2p = ctx.planes(g2)
+        ctx.lin_grads([p + ".output.dense"], g2, f, g2p, fp)
+        dpre = Bk.linear_dx(ctx, g2, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=g2p)
+        dprep = ctx.planes(dpre)
+        ctx.lin_grads([p + ".intermediate.dense"], dpre, h1, dprep, h1p)
         # dh1 = ds2 + dpre W (a fresh buffer: the weight-gradient GEMM on the side stream may still be
         # reading ds2)
-        dh1 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", residual=ds2)
+        dh1 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", residual=ds2, dyp=dprep)
         ds1, ds1d = Bk.layernorm_bwd(ctx, dh1, s1, p + ".attention.output.LayerNorm", m1, r1, drop_site=s + ".attn_out")
         g1 = ds1d if ds1d is not None else ds1
-        ctx.lin_grads([p + ".attention.output.dense"], g1, Bk.as2d(o))
-        do = Bk.linear_dx(ctx, g1, p + ".attention.output.dense").view(o.shape)
+        g1p = ctx.planes(g1)
+        ctx.lin_grads([p + ".attention.output.dense"], g1, Bk.as2d(o), g1p, op)
+        do = Bk.linear_dx(ctx, g1, p + ".attention.output.dense", dyp=g1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
         K.attn_bwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], o, lse, do, H, key_bias=st["kb"],
                    dq=dqkv[..., :D], dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:], **attn_drop)
         names = [p + ".attention.self.query", p + ".attention.self.key", p + ".attention.self.value"]
         dq2 = Bk.as2d(dqkv)
-        ctx.lin_grads(names, dq2, x)
+        dq2p = ctx.planes(dq2)
+        ctx.lin_grads(names, dq2, x, dq2p, xp)
         Wp, _ = ctx.w_packed(names)
-        dx = Bk.linear_dx(ctx, dq2, Wp, residual=ds1)  # dx_in = ds1 + dQKV [Wq;Wk;Wv] (fresh buffer)
+        dx = Bk.linear_dx(ctx, dq2, Wp, residual=ds1, dyp=dq2p)  # dx_in = ds1 + dQKV [Wq;Wk;Wv] (fresh buffer)
         ctx.flush_ready()
     # embeddings: undo the embedding dropout, LayerNorm backward, scatter into the tables
     if st["emb_drop"]:
@@ -324,15 +335,19 @@ def vit_forward(ctx: Bk.StepCtx, cfg: ViTConfig, px, keep):
     for i in range(cfg.num_hidden_layers):
         p = f"encoder.layer.{i}"
         h, mb, rb = Bk.layernorm(ctx, x, p + ".layernorm_before", eps)
+        hp = ctx.planes(h) if keep else None  # split once, kept for the weight-gradient GEMM (see BERT)
         qkv = Bk.linear_packed(ctx, h, [p + ".attention.attention.query", p + ".attention.attention.key",
-                                        p + ".attention.attention.value"]).view(B, T, 3 * D)
+                                        p + ".attention.attention.value"], xp=hp).view(B, T, 3 * D)
         o, lse = K.attn_fwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], H)
-        x1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x)
+        op = ctx.planes(Bk.as2d(o)) if keep else None
+        x1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, xp=op)
         h2, ma, ra = Bk.layernorm(ctx, x1, p + ".layernorm_after", eps)
-        f, pre = Bk.linear(ctx, h2, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep)
-        x2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=x1)
+        h2p = ctx.planes(h2) if keep else None
+        f, pre = Bk.linear(ctx, h2, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h2p)
+        fp = ctx.planes(f) if keep else None
+        x2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=x1, xp=fp)
         if keep:
-            states.append((x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f))
+            states.append((x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f, (hp, op, h2p, fp)))
         x = x2
     y, mf, rf = Bk.layernorm(ctx, x, "layernorm", eps)
     st = dict(patches=patches, layers=states, x_last=x, mf=mf, rf=rf, B=B, T=T) if keep else None
@@ -344,22 +359,26 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
     dx, _ = Bk.layernorm_bwd(ctx, Bk.as2d(dout).contiguous(), st["x_last"], "layernorm", st["mf"], st["rf"])
     for i in reversed(range(cfg.num_hidden_layers)):
         p = f"encoder.layer.{i}"
-        x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f = st["layers"][i]
-        ctx.lin_grads([p + ".output.dense"], dx, f)
-        dpre = Bk.linear_dx(ctx, dx, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre)
-        ctx.lin_grads([p + ".intermediate.dense"], dpre, h2)
-        dh2 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense")
+        x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f, (hp, op, h2p, fp) = st["layers"][i]
+        dxp = ctx.planes(dx)
+        ctx.lin_grads([p + ".output.dense"], dx, f, dxp, fp)
+        dpre = Bk.linear_dx(ctx, dx, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=dxp)
+        dprep = ctx.planes(dpre)
+        ctx.lin_grads([p + ".intermediate.dense"], dpre, h2, dprep, h2p)
+        dh2 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", dyp=dprep)
         dx1, _ = Bk.layernorm_bwd(ctx, dh2, x1, p + ".layernorm_after", ma, ra, dx_add=dx)
-        ctx.lin_grads([p + ".attention.output.dense"], dx1, Bk.as2d(o))
-        do = Bk.linear_dx(ctx, dx1, p + ".attention.output.dense").view(o.shape)
+        dx1p = ctx.planes(dx1)
+        ctx.lin_grads([p + ".attention.output.dense"], dx1, Bk.as2d(o), dx1p, op)
+        do = Bk.linear_dx(ctx, dx1, p + ".attention.output.dense", dyp=dx1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
         K.attn_bwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], o, lse, do, H, dq=dqkv[..., :D],
                    dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:])
         names = [p + ".attention.attention.query", p + ".attention.attention.key", p + ".attention.attention.value"]
         dq2 = Bk.as2d(dqkv)
-        ctx.lin_grads(names, dq2, h)
+        dq2p = ctx.planes(dq2)
+        ctx.lin_grads(names, dq2, h, dq2p, hp)
         Wp, _ = ctx.w_packed(names)
-        dh = Bk.linear_dx(ctx, dq2, Wp)
+        dh = Bk.linear_dx(ctx, dq2, Wp, dyp=dq2p)
         dx, _ = Bk.layernorm_bwd(ctx, dh, x, p + ".layernorm_before", mb, rb, dx_add=dx1)
         ctx.flush_ready()
     dpatch, dcls, dpos = K.vit_tokens_bwd(dx.view(st["B"], st["T"], D))

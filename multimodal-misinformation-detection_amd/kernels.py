@@ -59,6 +59,7 @@ class GemmArgs(ctypes.Structure):
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("splits", ctypes.c_int),
         ("a_rowsum", ctypes.c_void_p), ("a_rowsum_beta", ctypes.c_float),
+        ("a_planes", ctypes.c_void_p), ("b_planes", ctypes.c_void_p),
     ]
 
 
@@ -108,6 +109,9 @@ SIGNATURES = {
     "mmfd_dropout_hash": (ctypes.c_uint32, [_U64, _U64, _U64]),
     "mmfd_gemm": (_I, [ctypes.POINTER(GemmArgs), _VP]),
     "mmfd_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmArgs)]),
+    "mmfd_set_fp32_gemm_mode": (_I, [_I]),
+    "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
+    "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
     "mmfd_colsum": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _F, _VP, _I64, _VP]),
     "mmfd_attn_fwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
     "mmfd_attn_bwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
@@ -300,16 +304,51 @@ class GemmProbe:
         return out
 
 
+def _x6(a):
+    """whether mmfd_gemm runs this fp32 product on split bf16 operands (gemm.hip x6_plan)"""
+    if fp32_gemm_mode() != 1 or a.dtype != F32 or a.c_dtype != F32:
+        return False
+    ra, ca = (a.K, a.M) if a.trans_a else (a.M, a.K)
+    rb, cb = (a.K, a.N) if a.trans_b else (a.N, a.K)
+    if ca % 8 or cb % 8 or ((a.trans_a or a.trans_b) and a.K % 64):
+        return False
+    return 6 * max(ra * ca, rb * cb) < (1 << 31) - 4096
+
+
+_FP32_MODE = None
+
+
+def set_fp32_gemm_mode(mode):
+    """fp32 GEMMs: 'split' (bf16 operand planes, six MFMA products, fp32 accumulation; the default)
+    or 'native' (fp32 MFMA). Returns the previous mode name."""
+    global _FP32_MODE
+    code = {"native": 0, "split": 1}[mode]
+    old = lib().mmfd_set_fp32_gemm_mode(code)
+    _check(0 if old >= 0 else old, "mmfd_set_fp32_gemm_mode")
+    _FP32_MODE = code
+    return {0: "native", 1: "split"}[old]
+
+
+def fp32_gemm_mode():
+    global _FP32_MODE
+    if _FP32_MODE is None:  # the library's load-time default (env MMFD_FP32_GEMM)
+        old = lib().mmfd_set_fp32_gemm_mode(1)
+        lib().mmfd_set_fp32_gemm_mode(old)
+        _FP32_MODE = old
+    return _FP32_MODE
+
+
 def _kernel_name(a, split):
     """the device kernel mmfd_gemm launches for these arguments (rocprof's demangled name)"""
     t = {F32: "float", BF16: "__bf16"}
     narrow = a.M >= 4096 and (a.N <= 128 or a.K < 64)  # gemm.hip use_g8
     g8 = not narrow and (a.dtype == BF16 or a.c_dtype == F32)
-    if g8:  # 256x256 kernel; PRE = one prefetched bf16 epilogue operand stream
+    if g8:  # 256x256 kernel; PRE = one prefetched bf16 epilogue operand stream; X6 = split operands
         streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD)) + int(a.beta != 0.0)
         pre = a.c_dtype == BF16 and streams == 1 and not split
-        base = (f"gemm256_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
-                f"{'true' if pre else 'false'}>")
+        x6 = _x6(a)
+        base = (f"gemm256_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
+                f"{'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
     else:
         base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")
@@ -317,10 +356,11 @@ def _kernel_name(a, split):
 
 def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
          residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0, a_rowsum=None,
-         a_rowsum_beta=0.0, residual_first=False):
+         a_rowsum_beta=0.0, residual_first=False, a_planes=None, b_planes=None):
     """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
     nn.Linear weight) when trans_b=False, else B ([K,N] stored). `a_rowsum` (fp32 [M]) additionally
-    receives a_rowsum_beta * a_rowsum + sum_k op(A)[m, k] (bias gradient of a weight-gradient GEMM)."""
+    receives a_rowsum_beta * a_rowsum + sum_k op(A)[m, k] (bias gradient of a weight-gradient GEMM).
+    `a_planes` / `b_planes`: split3() of the stored fp32 A / B, reused by the split-operand fp32 GEMM."""
     _require_cuda(A, B, out, bias, residual, aux)
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
@@ -356,7 +396,7 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
         e0.record()
     _ops().gemm(A, B, bool(trans_a), bool(trans_b), out, float(alpha), float(beta), bias, residual,
                 bool(residual_first), int(act), aux, float(dropout_p), seed.t if seed is not None else None,
-                _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta))
+                _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta), a_planes, b_planes)
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
@@ -379,7 +419,25 @@ def _probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits):
     if residual is not None:
         a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
     a.ep.act = int(act)
-    return _kernel_name(a, lib().mmfd_gemm_workspace_bytes(ctypes.byref(a)) > 0)
+    return _kernel_name(a, lib().mmfd_gemm_splits(ctypes.byref(a)) > 1)
+
+
+def split3(x, out=None):
+    """fp32 [rows, cols] (row-major view, cols % 8 == 0) -> bf16 planes [3, rows, cols]: hi = bf16(x),
+    mid = bf16(x - hi), lo = bf16(x - hi - mid) — the operand form of the split-operand fp32 GEMM"""
+    _require_cuda(x)
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise TypeError("split3 takes a 2-D fp32 tensor")
+    if out is None:
+        out = torch.empty((3, x.shape[0], x.shape[1]), device=x.device, dtype=torch.bfloat16)
+    _ops().split3(x, out)
+    return out
+
+
+def split_eligible(x):
+    """whether GEMMs on fp32 operand `x` run on split planes (mode split, 16-B plane rows)"""
+    return (x is not None and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] % 8 == 0
+            and x.stride(1) == 1 and fp32_gemm_mode() == 1 and 6 * x.numel() < (1 << 31) - 4096)
 
 
 def colsum(X, out=None, beta=0.0):

@@ -209,6 +209,12 @@ class FusionTrainer:
         self._graph = g
         return self
 
+    def release_graph(self):
+        """drop the captured step and its private memory pool (eager steps afterwards)"""
+        self._graph = self._graph_loss = None
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
     def replay(self, batch=None):
         """one captured training step; returns the (static) device loss vector"""
         if batch is not None and batch is not self._static:

@@ -445,3 +445,70 @@ def test_adamw_matches_torch():
     torch.cuda.synchronize()
     for r, d in zip(ref, dev):
         assert (r.detach() - d.detach().cpu()).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+@pytest.mark.parametrize("shape", [(512, 768, 768), (1000, 520, 200), (768, 256, 4096), (256, 2304, 65536)])
+def test_gemm_fp32_split_operands_error_matches_fp32_mfma(layout, shape):
+    """fp32 GEMMs on split bf16 operands (x = hi + mid + lo, six products accumulated small-first,
+    include/mmfd.h mmfd_set_fp32_gemm_mode) against an fp64 product: the error may not exceed the
+    fp32 MFMA's own on the same inputs by more than 1.5x (+1e-7 of the output scale); covers
+    ragged M/N tiles, K not a multiple of 64 (K-contiguous operands only), split-K over the six
+    segments (the tall K = 65536 weight-gradient shape) and every operand layout."""
+    M, N, Kd = shape
+    ta, tb = layout[0] == "t", layout[1] == "t"
+    if (ta or tb) and Kd % 64:
+        pytest.skip("MN-contiguous operands need whole 64-row K tiles on the split path (fp32 MFMA used)")
+    g = torch.Generator().manual_seed(M + N + Kd)
+    A = torch.randn((Kd, M) if ta else (M, Kd), generator=g).to(DEV)
+    B = (torch.randn((Kd, N) if tb else (N, Kd), generator=g) * 0.05).to(DEV)
+    ref = (A.double().T if ta else A.double()) @ (B.double() if tb else B.double().T)
+    outs = {}
+    old = K.set_fp32_gemm_mode("split")
+    try:
+        for mode in ("split", "native"):
+            K.set_fp32_gemm_mode(mode)
+            outs[mode] = K.gemm(A, B, trans_a=ta, trans_b=tb)
+        torch.cuda.synchronize()
+    finally:
+        K.set_fp32_gemm_mode(old)
+    scale = ref.abs().max().item()
+    err = {m: (o.double() - ref).abs().max().item() / scale for m, o in outs.items()}
+    assert err["split"] <= 1.5 * err["native"] + 1e-7, err
+    assert err["split"] <= 1e-5 * math.sqrt(Kd / 768), err
+
+
+def test_gemm_fp32_split_operands_epilogues_rowsum():
+    """the split path keeps the fp32 epilogues (bias, GELU + saved pre-activation, residual, dropout,
+    beta) and the fused bias-gradient row sums of op(A), with and without split-K"""
+    old = K.set_fp32_gemm_mode("split")
+    try:
+        M, N, Kd = 520, 768, 384
+        x = _rand(M, Kd, seed=51).to(DEV); w = _rand(N, Kd, seed=52, scale=0.1).to(DEV)
+        b = _rand(N, seed=53).to(DEV); res = _rand(M, N, seed=54).to(DEV)
+        base = x.double() @ w.double().T + b.double()
+        aux = torch.empty(M, N, device=DEV)
+        y = K.gemm(x, w, bias=b, act=K.ACT_GELU, aux=aux)
+        assert (aux.double() - base).abs().max().item() <= 2e-5
+        assert (y.double() - torch.nn.functional.gelu(base)).abs().max().item() <= 2e-5
+        y = K.gemm(x, w, bias=b, residual=res)
+        assert (y.double() - base - res.double()).abs().max().item() <= 2e-5
+        c0 = res.clone()
+        K.gemm(x, w, out=c0, beta=1.0)
+        assert (c0.double() - (x.double() @ w.double().T + res.double())).abs().max().item() <= 2e-5
+        seed = K.Seed(11)
+        yd = K.gemm(x, w, dropout_p=0.1, seed=seed, salt=K.salt_of("x6"))
+        K.set_fp32_gemm_mode("native")
+        yn = K.gemm(x, w, dropout_p=0.1, seed=seed, salt=K.salt_of("x6"))
+        K.set_fp32_gemm_mode("split")
+        assert torch.equal(yd == 0, yn == 0)  # same counter-hash mask
+        for Mt, splits in ((2048, 0), (2048, 4)):  # weight gradient dW = dY^T X with its bias gradient
+            dy = _rand(Mt, 256, seed=55).to(DEV); xx = _rand(Mt, 512, seed=56).to(DEV)
+            rs = torch.full((256,), 0.5, device=DEV)
+            dw = K.gemm(dy, xx, trans_a=True, trans_b=True, splits=splits, a_rowsum=rs, a_rowsum_beta=1.0)
+            torch.cuda.synchronize()
+            ref = dy.double().T @ xx.double()
+            assert (dw.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+            assert (rs.double() - (0.5 + dy.double().sum(0))).abs().max().item() <= 1e-4
+    finally:
+        K.set_fp32_gemm_mode(old)

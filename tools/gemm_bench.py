@@ -1,5 +1,5 @@
 """GEMM throughput on the hot-path shapes (BERT M=65536, ViT M=100864 tokens at bs=256 pairs).
-python tools/gemm_bench.py [--dtype bf16|fp32] [--iters N]"""
+python tools/gemm_bench.py [--dtype bf16|fp32] [--fp32-mode split|native] [--iters N]"""
 import argparse
 import os
 import sys
@@ -51,7 +51,9 @@ if __name__ == "__main__":
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", action="store_true", help="also time torch.matmul (hipBLASLt)")
+    ap.add_argument("--fp32-mode", default="split", choices=["split", "native"])
     a = ap.parse_args()
+    K.set_fp32_gemm_mode(a.fp32_mode)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     tot_ms = tot_f = 0.0
     for name, M in (("bert", 65536), ("vit", 100864)):
