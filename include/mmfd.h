@@ -72,6 +72,9 @@ typedef struct mmfd_epilogue {
   uint64_t salt;           /* call-site id; element index = m * N + n */
   int residual_first;      /* 1: z += residual BEFORE the (forward) activation, i.e. act(acc + bias +
                               residual) — the ResNet bottleneck's relu(bn3(conv3) + identity) */
+  void* out_planes;        /* fp32 C only: bf16 [3][M][N] split planes of the final output (mmfd_split3
+                              form, N % 8 == 0), written beside C, or instead of it when C is NULL
+                              (beta = 0): a GEMM output whose only consumers are split-operand GEMMs */
 } mmfd_epilogue;
 
 typedef struct mmfd_gemm_args {

@@ -304,14 +304,25 @@ def as2d(x):
 # linear
 # -------------------------------------------------------------------------------------------------
 def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=None, drop_site=None,
-           out_dtype=None, xp=None):
+           out_dtype=None, xp=None, out_planes=None, write_out=True):
     W = ctx.w(name)
     aux = None
     if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
         aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
     y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,
-               a_planes=xp, **(ctx.drop(drop_site) if drop_site else {}))
+               a_planes=xp, out_planes=out_planes, write_out=write_out, **(ctx.drop(drop_site) if drop_site else {}))
     return y, aux
+
+
+def out_planes(ctx: StepCtx, rows, cols, consumers, device):
+    """(planes, write_out) for a GEMM output in split-operand fp32 mode: bf16 [3, rows, cols]
+    written by the producing epilogue, and whether the fp32 output is needed at all — it is not
+    when every consumer GEMM ((M, N, K, trans_a, trans_b) tuples) runs on split operands.
+    (None, True) otherwise."""
+    if ctx.dt != torch.float32 or K.fp32_gemm_mode() != 1 or cols % 8 or os.environ.get("MMFD_NO_EPI_PLANES"):
+        return None, True
+    pl = torch.empty((3, rows, cols), device=device, dtype=torch.bfloat16)
+    return pl, not all(K.x6_ok(*c) for c in consumers)
 
 
 def linear_packed(ctx: StepCtx, x2d, names, xp=None):
@@ -320,10 +331,11 @@ def linear_packed(ctx: StepCtx, x2d, names, xp=None):
 
 
 def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
-              residual=None, dyp=None):
+              residual=None, dyp=None, out_planes=None, write_out=True):
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
     return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
-                  residual=residual, a_planes=dyp, **(ctx.drop(drop_site) if drop_site else {}))
+                  residual=residual, a_planes=dyp, out_planes=out_planes, write_out=write_out,
+                  **(ctx.drop(drop_site) if drop_site else {}))
 
 
 # -------------------------------------------------------------------------------------------------

@@ -42,7 +42,31 @@ struct EpiArgs {
   float beta;
   int vec;  // host-checked: C / residual / aux 16-B aligned with leading dims multiple of 8
   int res_first;  // residual added before the forward activation
+  // fp32 C only: the output's bf16 split planes [3][M][N] (hi, mid, lo; see split3_kernel) written
+  // beside C or instead of it (c_out = 0) — the operand form of the next split-operand GEMM
+  bf16* pl; int64_t pl_stride; int c_out;
 };
+
+__device__ __forceinline__ void split1(float x, bf16& h, bf16& m, bf16& l) {
+  h = (bf16)x;
+  const float r = x - (float)h;
+  m = (bf16)r;
+  l = (bf16)(r - (float)m);
+}
+// 8 consecutive outputs of row `row` into the planes (16-B stores)
+__device__ __forceinline__ void planes_store8(const EpiArgs& e, int64_t N, int64_t row, int64_t col, const float (&z)[8]) {
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    bf16 a, b, c;
+    split1(z[u], a, b, c);
+    h[u] = a; m[u] = b; l[u] = c;
+  }
+  bf16* d = e.pl + row * N + col;
+  *reinterpret_cast<uint4*>(d) = __builtin_bit_cast(uint4, h);
+  *reinterpret_cast<uint4*>(d + e.pl_stride) = __builtin_bit_cast(uint4, m);
+  *reinterpret_cast<uint4*>(d + 2 * e.pl_stride) = __builtin_bit_cast(uint4, l);
+}
 
 template <typename TC>
 __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t ldc, int64_t N,
@@ -66,6 +90,13 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& e, TC* C, int64_t 
   if (e.residual && !e.res_first) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
   TC* cp = C + row * ldc + col;
   if (e.beta != 0.0f) z += e.beta * to_f32(*cp);
+  if (std::is_same<TC, float>::value && e.pl) {
+    bf16 h, m, l;
+    split1(z, h, m, l);
+    bf16* d = e.pl + row * N + col;
+    d[0] = h; d[e.pl_stride] = m; d[2 * e.pl_stride] = l;
+    if (!e.c_out) return;
+  }
   *cp = from_f32<TC>(z);
 }
 
@@ -169,6 +200,10 @@ __device__ __forceinline__ void epilogue_store8(const EpiArgs& e, TC* C, int64_t
     V8<TC>::load(cp, c);
 #pragma unroll
     for (int q = 0; q < 8; ++q) z[q] += e.beta * c[q];
+  }
+  if (std::is_same<TC, float>::value && e.pl) {
+    planes_store8(e, N, row, col, z);
+    if (!e.c_out) return;
   }
   V8<TC>::store(cp, z);
 }
@@ -946,6 +981,10 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 #pragma unroll
             for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
           }
+          if (std::is_same<TC, float>::value && e.pl) {
+            planes_store8(e, N, rbase + lr0 + kk * rstep, col, z);
+            if (!e.c_out) continue;
+          }
           V8<TC>::store(cp + kk * cs, z);
         }
       }
@@ -1312,7 +1351,10 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "mmfd_gemm: bad dtype %d", a.dtype);
   MMFD_CHECK_ARG(a.c_dtype == MMFD_F32 || a.c_dtype == MMFD_BF16, "mmfd_gemm: bad c_dtype %d", a.c_dtype);
   MMFD_CHECK_ARG(a.M >= 0 && a.N >= 0 && a.K >= 0, "mmfd_gemm: negative shape");
-  MMFD_CHECK_ARG(a.C != nullptr, "mmfd_gemm: null C");
+  MMFD_CHECK_ARG(a.C != nullptr || (a.ep.out_planes != nullptr && a.c_dtype == MMFD_F32 && a.beta == 0.f),
+                 "mmfd_gemm: null C (allowed only with fp32 out_planes and beta = 0)");
+  MMFD_CHECK_ARG(a.ep.out_planes == nullptr || (a.N % 8 == 0 && ((uintptr_t)a.ep.out_planes & 15) == 0),
+                 "mmfd_gemm: out_planes need N %% 8 == 0 and 16-B alignment");
   MMFD_CHECK_ARG(a.ldc >= a.N, "mmfd_gemm: ldc %lld < N %lld", (long long)a.ldc, (long long)a.N);
   const int act = a.ep.act;
   MMFD_CHECK_ARG(act >= 0 && act <= MMFD_ACT_SIGMOID, "mmfd_gemm: bad act %d", act);
@@ -1328,9 +1370,12 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   e.ldaux = a.ep.ldaux; e.act = act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
   e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
   e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta; e.res_first = a.ep.residual_first ? 1 : 0;
+  e.pl = a.c_dtype == MMFD_F32 ? (bf16*)a.ep.out_planes : nullptr;
+  e.pl_stride = a.M * a.N;
+  e.c_out = (a.C != nullptr) ? 1 : 0;
   {
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    bool v = al(a.C) && (a.ldc % 8) == 0;
+    bool v = (a.C == nullptr || al(a.C)) && (a.ldc % 8) == 0;
     if (a.ep.residual) v = v && al(a.ep.residual) && (a.ep.ldr % 8) == 0;
     if (a.ep.aux) v = v && al(a.ep.aux) && (a.ep.ldaux % 8) == 0;
     if (a.ep.bias) v = v && al(a.ep.bias);
@@ -1354,7 +1399,10 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
 
   // split-operand fp32 GEMM only with the full workspace it asked for (else the fp32 MFMA path)
   X6Plan xp = x6_plan(a);
-  if (xp.on && (a.workspace == nullptr || a.workspace_bytes < mmfd_gemm_workspace_bytes(&a))) xp.on = false;
+  if (xp.on) {  // (no workspace at all when both operands come split and there is no split-K)
+    const int64_t wneed = mmfd_gemm_workspace_bytes(&a);
+    if (wneed > 0 && (a.workspace == nullptr || a.workspace_bytes < wneed)) xp.on = false;
+  }
   int64_t need = 0;
   int splits = choose_splits(a, &need, xp.on);
   if (!xp.on && splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need + rowsum_ws_bytes(a, splits, use_g8(a)))) {

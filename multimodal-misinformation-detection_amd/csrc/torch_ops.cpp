@@ -53,7 +53,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
           bool residual_first, int64_t act, const std::optional<at::Tensor>& aux, double dropout_p,
           const std::optional<at::Tensor>& seed, int64_t salt, int64_t splits, const std::optional<at::Tensor>& a_rowsum,
           double a_rowsum_beta, const std::optional<at::Tensor>& a_planes = std::nullopt,
-          const std::optional<at::Tensor>& b_planes = std::nullopt) {
+          const std::optional<at::Tensor>& b_planes = std::nullopt,
+          const std::optional<at::Tensor>& out_planes = std::nullopt, bool write_out = true) {
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "mmfd::gemm operands must share a dtype");
   mmfd_gemm_args a{};
   a.dtype = dtype_code(A);
@@ -90,6 +91,14 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
   };
   a.a_planes = planes(a_planes, A, "a_planes");
   a.b_planes = planes(b_planes, B, "b_planes");
+  if (out_planes.has_value() && out_planes->defined()) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat, "mmfd::gemm: out_planes need an fp32 output");
+    a.ep.out_planes = const_cast<void*>(planes(out_planes, out, "out_planes"));
+  }
+  if (!write_out) {
+    TORCH_CHECK(a.ep.out_planes != nullptr && beta == 0.0, "mmfd::gemm: write_out=False needs out_planes and beta = 0");
+    a.C = nullptr; a.ldc = a.N;
+  }
   const int64_t need = mmfd_gemm_workspace_bytes(&a);
   at::Tensor ws;
   if (need > 0) {
@@ -271,7 +280,8 @@ void topk(const at::Tensor& scores, int64_t k, at::Tensor& values, at::Tensor& i
 TORCH_LIBRARY(mmfd, m) {
   m.def("gemm(Tensor A, Tensor B, bool trans_a, bool trans_b, Tensor(a!) out, float alpha, float beta, Tensor? bias, "
         "Tensor? residual, bool residual_first, int act, Tensor(b!)? aux, float dropout_p, Tensor? seed, int salt, "
-        "int splits, Tensor(c!)? a_rowsum, float a_rowsum_beta, Tensor? a_planes=None, Tensor? b_planes=None) -> ()");
+        "int splits, Tensor(c!)? a_rowsum, float a_rowsum_beta, Tensor? a_planes=None, Tensor? b_planes=None, "
+        "Tensor(d!)? out_planes=None, bool write_out=True) -> ()");
   m.def("split3(Tensor x, Tensor(a!) planes) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, int act=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) out, Tensor(b!) lse, int heads, float scale, "

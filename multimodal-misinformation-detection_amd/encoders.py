@@ -159,8 +159,13 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
                           xp=op)
         h1, m1, r1 = Bk.layernorm(ctx, s1, p + ".attention.output.LayerNorm", eps)
         h1p = ctx.planes(h1) if keep else None
-        f, pre = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h1p)
-        fp = ctx.planes(f) if keep else None
+        T_, I_ = h1.shape[0], cfg.intermediate_size
+        # the GELU output feeds only the FFN2 forward and FFN2 weight-gradient GEMMs: its planes come
+        # from the FFN1 epilogue, and the fp32 copy is skipped when both run on split operands
+        fp, f_out = Bk.out_planes(ctx, T_, I_, [(T_, D, I_), (D, I_, T_, True, True)], h1.device) if keep \
+            else (None, True)
+        f, pre = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h1p,
+                           out_planes=fp, write_out=f_out)
         s2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=h1, drop_site=s + ".ffn_out", xp=fp)
         x_out, m2, r2 = Bk.layernorm(ctx, s2, p + ".output.LayerNorm", eps)
         if keep:
@@ -182,8 +187,10 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         g2 = ds2d if ds2d is not None else ds2
         g2p = ctx.planes(g2)
         ctx.lin_grads([p + ".output.dense"], g2, f, g2p, fp)
-        dpre = Bk.linear_dx(ctx, g2, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=g2p)
-        dprep = ctx.planes(dpre)
+        T_, I_ = g2.shape[0], cfg.intermediate_size
+        dprep, dpre_out = Bk.out_planes(ctx, T_, I_, [(I_, D, T_, True, True), (T_, D, I_, False, True)], g2.device)
+        dpre = Bk.linear_dx(ctx, g2, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=g2p, out_planes=dprep,
+                            write_out=dpre_out)
         ctx.lin_grads([p + ".intermediate.dense"], dpre, h1, dprep, h1p)
         # dh1 = ds2 + dpre W (a fresh buffer: the weight-gradient GEMM on the side stream may still be
         # reading ds2)
@@ -343,8 +350,11 @@ def vit_forward(ctx: Bk.StepCtx, cfg: ViTConfig, px, keep):
         x1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, xp=op)
         h2, ma, ra = Bk.layernorm(ctx, x1, p + ".layernorm_after", eps)
         h2p = ctx.planes(h2) if keep else None
-        f, pre = Bk.linear(ctx, h2, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h2p)
-        fp = ctx.planes(f) if keep else None
+        T_, I_ = h2.shape[0], cfg.intermediate_size
+        fp, f_out = Bk.out_planes(ctx, T_, I_, [(T_, D, I_), (D, I_, T_, True, True)], h2.device) if keep \
+            else (None, True)  # GELU output planes from the FFN1 epilogue (see BERT)
+        f, pre = Bk.linear(ctx, h2, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h2p,
+                           out_planes=fp, write_out=f_out)
         x2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=x1, xp=fp)
         if keep:
             states.append((x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f, (hp, op, h2p, fp)))
@@ -362,8 +372,10 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
         x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f, (hp, op, h2p, fp) = st["layers"][i]
         dxp = ctx.planes(dx)
         ctx.lin_grads([p + ".output.dense"], dx, f, dxp, fp)
-        dpre = Bk.linear_dx(ctx, dx, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=dxp)
-        dprep = ctx.planes(dpre)
+        T_, I_ = dx.shape[0], cfg.intermediate_size
+        dprep, dpre_out = Bk.out_planes(ctx, T_, I_, [(I_, D, T_, True, True), (T_, D, I_, False, True)], dx.device)
+        dpre = Bk.linear_dx(ctx, dx, p + ".output.dense", act=K.ACT_GELU_BWD, aux=pre, dyp=dxp, out_planes=dprep,
+                            write_out=dpre_out)
         ctx.lin_grads([p + ".intermediate.dense"], dpre, h2, dprep, h2p)
         dh2 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", dyp=dprep)
         dx1, _ = Bk.layernorm_bwd(ctx, dh2, x1, p + ".layernorm_after", ma, ra, dx_add=dx)

@@ -44,6 +44,7 @@ class EpilogueArgs(ctypes.Structure):
         ("seed", ctypes.c_void_p),
         ("salt", ctypes.c_uint64),
         ("residual_first", ctypes.c_int),
+        ("out_planes", ctypes.c_void_p),
     ]
 
 
@@ -356,11 +357,14 @@ def _kernel_name(a, split):
 
 def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=1.0, beta=0.0, bias=None,
          residual=None, act=ACT_NONE, aux=None, dropout_p=0.0, seed=None, salt=0, splits=0, a_rowsum=None,
-         a_rowsum_beta=0.0, residual_first=False, a_planes=None, b_planes=None):
+         a_rowsum_beta=0.0, residual_first=False, a_planes=None, b_planes=None, out_planes=None, write_out=True):
     """C = epilogue(alpha * op(A) @ op(B)) with op(A) = A or A^T ([M,K]) and op(B) = B^T ([N,K] stored,
     nn.Linear weight) when trans_b=False, else B ([K,N] stored). `a_rowsum` (fp32 [M]) additionally
     receives a_rowsum_beta * a_rowsum + sum_k op(A)[m, k] (bias gradient of a weight-gradient GEMM).
-    `a_planes` / `b_planes`: split3() of the stored fp32 A / B, reused by the split-operand fp32 GEMM."""
+    `a_planes` / `b_planes`: split3() of the stored fp32 A / B, reused by the split-operand fp32 GEMM.
+    `out_planes` (bf16 [3, M, N], fp32 output only): the output's split planes, written by the
+    epilogue; with write_out=False instead of `out` (which then only carries the shape and stays
+    unwritten — only for outputs read by split-operand GEMMs alone, see x6_ok)."""
     _require_cuda(A, B, out, bias, residual, aux)
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
@@ -396,7 +400,8 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
         e0.record()
     _ops().gemm(A, B, bool(trans_a), bool(trans_b), out, float(alpha), float(beta), bias, residual,
                 bool(residual_first), int(act), aux, float(dropout_p), seed.t if seed is not None else None,
-                _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta), a_planes, b_planes)
+                _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta), a_planes, b_planes, out_planes,
+                bool(write_out))
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
@@ -432,6 +437,20 @@ def split3(x, out=None):
         out = torch.empty((3, x.shape[0], x.shape[1]), device=x.device, dtype=torch.bfloat16)
     _ops().split3(x, out)
     return out
+
+
+def x6_ok(M, N, K, trans_a=False, trans_b=False):
+    """whether mmfd_gemm runs this fp32 product on split operands (gemm.hip x6_plan + use_g8 +
+    mfma_ok for contiguous operands)"""
+    if fp32_gemm_mode() != 1 or min(M, N, K) < 16:
+        return False
+    if M >= 4096 and (N <= 128 or K < 64):
+        return False
+    ra, ca = (K, M) if trans_a else (M, K)
+    rb, cb = (K, N) if trans_b else (N, K)
+    if ca % 8 or cb % 8 or ((trans_a or trans_b) and K % 64):
+        return False
+    return 6 * max(ra * ca, rb * cb) < (1 << 31) - 4096
 
 
 def split_eligible(x):

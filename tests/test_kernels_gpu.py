@@ -512,3 +512,37 @@ def test_gemm_fp32_split_operands_epilogues_rowsum():
             assert (rs.double() - (0.5 + dy.double().sum(0))).abs().max().item() <= 1e-4
     finally:
         K.set_fp32_gemm_mode(old)
+
+
+@pytest.mark.parametrize("case", ["fast", "ragged", "splitk", "gelu_bwd"])
+def test_gemm_out_planes_equal_split_of_output(case):
+    """the epilogue's split planes (out_planes) are bit-identical to split3 of the fp32 output it
+    writes, on the full-tile fast path, the per-element path (ragged tiles), the split-K reduce and
+    with the GELU-backward epilogue; write_out=False leaves the fp32 output untouched"""
+    old = K.set_fp32_gemm_mode("split")
+    try:
+        if case == "splitk":
+            A = _rand(4096, 256, seed=61).to(DEV); B = _rand(4096, 512, seed=62).to(DEV)
+            kw = dict(trans_a=True, trans_b=True, splits=4)
+            M, N = 256, 512
+        else:
+            M, N, Kd = (1024, 768, 512) if case != "ragged" else (1000, 776, 200)
+            A = _rand(M, Kd, seed=63).to(DEV); B = _rand(N, Kd, seed=64, scale=0.1).to(DEV)
+            kw = dict(bias=_rand(N, seed=65).to(DEV))
+            if case == "gelu_bwd":
+                kw = dict(act=K.ACT_GELU_BWD, aux=_rand(M, N, seed=66).to(DEV))
+        ref = K.gemm(A, B, **kw)
+        pl = torch.empty((3, M, N), device=DEV, dtype=torch.bfloat16)
+        out = torch.full((M, N), 7.0, device=DEV)
+        K.gemm(A, B, out=out, out_planes=pl, write_out=False, **kw)
+        both = torch.empty((3, M, N), device=DEV, dtype=torch.bfloat16)
+        out2 = K.gemm(A, B, out_planes=both, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(out2, ref)
+        assert torch.equal(pl.view(torch.int16), K.split3(ref).view(torch.int16))
+        assert torch.equal(both.view(torch.int16), pl.view(torch.int16))
+        assert bool((out == 7.0).all())
+        recon = pl[0].double() + pl[1].double() + pl[2].double()
+        assert (recon - ref.double()).abs().max().item() <= 2 ** -23 * ref.abs().max().item()
+    finally:
+        K.set_fp32_gemm_mode(old)

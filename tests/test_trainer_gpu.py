@@ -138,3 +138,12 @@ def test_captured_step_replays_equal_eager_steps(precision):
                      (tr_e.head, tr_g.head)):
         for (n, p), (_, q) in zip(m_e.named_parameters(), m_g.named_parameters()):
             assert (p - q).abs().max().item() <= 3 * lr + 1e-6, n
+
+
+@pytest.mark.parametrize("B", [2, 4])
+def test_train_step_fp32_split_operand_weight_grads(B):
+    """token counts that are whole 64-row tiles (B = 2, 4 pairs of 16 tokens): the weight-gradient
+    GEMMs run on split operands and the GELU output / its gradient exist only as epilogue-written
+    planes (no fp32 copy) — gradients still match the oracle at the fp32 bounds"""
+    tr, ref = build_pair("fp32", dropout=0.0)
+    compare_step(tr, ref, tiny_batch(B, seed=21), loss_tol=1e-3, grad_rtol=2e-3)
