@@ -160,6 +160,11 @@ typedef struct mmfd_attn_args {
                                       by exp(min(cos_logit_scale[h], cos_max_log)) while staged (bf16,
                                       Lk <= 256, rel_bias required); replaces mmfd_swin_qk_norm */
   float cos_max_log;
+  /* backward, fp32 only: bf16 split planes [3][B*Lq][3*H*D] (mmfd_split3 form) of the packed
+     gradient [dq | dk | dv] — dq, dk, dv must be the three column blocks of one contiguous
+     [B, Lq, 3*H*D] buffer starting at dq (Lq == Lk) — written beside it, or instead of it with
+     planes_only (no accumulate): the operand of the QKV data- and weight-gradient GEMMs */
+  void* dqkv_planes; int planes_only;
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);

@@ -292,7 +292,9 @@ class StepCtx:
         r = 0
         for n in names:
             rows = self.P[n + ".weight"].shape[0]
-            self._lin_grads([n], dy2d[:, r:r + rows], x2d, None, xp)
+            # (a planes-only gradient has no fp32 copy to slice: slice its planes instead)
+            self._lin_grads([n], dy2d[:, r:r + rows], x2d,
+                            dyp[:, :, r:r + rows].contiguous() if dyp is not None else None, xp)
             r += rows
 
 

@@ -43,7 +43,20 @@ struct AttnP {
   void* dv; int64_t dv_sb, dv_st;
   float* delta;
   int acc_dq, acc_dkv;
+  // fp32 backward: split planes of the packed [dq | dk | dv] buffer (base = dq), see mmfd_attn_args
+  bf16* pl; int64_t pl_stride; const float* pl_base; int pl_only;
 };
+
+// one fp32 gradient element into the planes at its offset in the packed buffer
+__device__ __forceinline__ void plane_put(const AttnP& p, const float* dst, float v) {
+  const int64_t off = dst - p.pl_base;
+  const bf16 h = (bf16)v;
+  const float r = v - (float)h;
+  const bf16 m = (bf16)r;
+  p.pl[off] = h;
+  p.pl[off + p.pl_stride] = m;
+  p.pl[off + 2 * p.pl_stride] = (bf16)(r - (float)m);
+}
 
 template <typename T, int D>
 struct AT {
@@ -907,6 +920,13 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
           T* pv = dvb + key * p.dv_st + d * 16 + li;
           float vk = dkv[2 * d + 1][r] * p.scale, vv = dkv[2 * d][r];
           if (p.acc_dkv) { vk += to_f32(*pk); vv += to_f32(*pv); }
+          if constexpr (std::is_same<T, float>::value) {
+            if (p.pl) {
+              plane_put(p, pk, vk);
+              plane_put(p, pv, vv);
+              if (p.pl_only) continue;
+            }
+          }
           *pk = from_f32<T>(vk);
           *pv = from_f32<T>(vv);
         }
@@ -1044,6 +1064,12 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
           T* pq = dqb + q * p.dq_st + d * 16 + li;
           float vq = dq[d][r] * p.scale;
           if (p.acc_dq) vq += to_f32(*pq);
+          if constexpr (std::is_same<T, float>::value) {
+            if (p.pl) {
+              plane_put(p, pq, vq);
+              if (p.pl_only) continue;
+            }
+          }
           *pq = from_f32<T>(vq);
         }
       }
@@ -1208,10 +1234,26 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const bool v2 = p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  p.pl = nullptr; p.pl_only = 0;
+  const int64_t W = 3 * a->H * a->D;
+  if (a->dqkv_planes) {
+    MMFD_CHECK_ARG(a->dtype == MMFD_F32 && a->Lq == a->Lk && a->dk == (const float*)a->dq + a->H * a->D &&
+                       a->dv == (const float*)a->dq + 2 * a->H * a->D && a->dq_st == W && a->dk_st == W &&
+                       a->dv_st == W && a->dq_sb == a->Lq * W && a->dk_sb == a->dq_sb && a->dv_sb == a->dq_sb,
+                   "attn_bwd: dqkv_planes need fp32 dq | dk | dv packed in one contiguous [B, L, 3*H*D] buffer");
+    MMFD_CHECK_ARG(!a->planes_only || (!a->accumulate_dq && !a->accumulate_dkv),
+                   "attn_bwd: planes_only excludes accumulate");
+    if (v2) {  // the v2 kernels write the planes from their stores
+      p.pl = (bf16*)a->dqkv_planes; p.pl_stride = p.B * p.Lq * W; p.pl_base = (const float*)a->dq;
+      p.pl_only = a->planes_only;
+    }
+  }
   if (v2 && a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd_v2<bf16, 64>(p, s); else launch_bwd_v2<bf16, 32>(p, s); }
   else if (v2) { if (a->D > 32) launch_bwd_v2<float, 64>(p, s); else launch_bwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_bwd");
+  if (a->dqkv_planes && !v2)  // the v1 kernels write fp32 only: split afterwards
+    return mmfd_split3(p.B * p.Lq, W, (const float*)a->dq, W, a->dqkv_planes, stream);
   return 0;
 }

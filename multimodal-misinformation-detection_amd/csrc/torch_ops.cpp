@@ -174,7 +174,8 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
               const at::Tensor& dout, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, int64_t heads, double scale,
               const std::optional<at::Tensor>& key_bias, const std::optional<at::Tensor>& rel_bias, int64_t rel_bias_sb,
               int64_t rel_bias_mod, double dropout_p, const std::optional<at::Tensor>& seed, int64_t salt,
-              bool accumulate_dq, bool accumulate_dkv) {
+              bool accumulate_dq, bool accumulate_dkv, const std::optional<at::Tensor>& dqkv_planes = std::nullopt,
+              bool planes_only = false) {
   mmfd_attn_args a = attn_args(q, k, v, heads, scale, key_bias, rel_bias, rel_bias_sb, rel_bias_mod, dropout_p, seed, salt);
   const void* p;
   head_view(o, "o", &p, &a.o_sb, &a.o_st); a.o = const_cast<void*>(p);
@@ -186,6 +187,13 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
   at::Tensor delta = at::empty({a.B, a.H, a.Lq}, q.options().dtype(at::kFloat));
   a.delta = delta.data_ptr<float>();
   a.accumulate_dq = accumulate_dq; a.accumulate_dkv = accumulate_dkv;
+  if (dqkv_planes.has_value() && dqkv_planes->defined()) {
+    TORCH_CHECK(dqkv_planes->scalar_type() == at::kBFloat16 && dqkv_planes->is_contiguous() &&
+                    dqkv_planes->numel() == 3 * a.B * a.Lq * 3 * a.H * a.D,
+                "mmfd::attn_bwd: dqkv_planes must be contiguous bf16 [3, B*L, 3*H*D]");
+    a.dqkv_planes = dqkv_planes->data_ptr();
+    a.planes_only = planes_only ? 1 : 0;
+  }
   check(mmfd_attn_bwd(&a, stream_of(q)), "mmfd::attn_bwd");
 }
 
@@ -289,7 +297,8 @@ TORCH_LIBRARY(mmfd, m) {
         "Tensor? cos_logit_scale, float cos_max_log) -> ()");
   m.def("attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dout, Tensor(a!) dq, Tensor(b!) dk, "
         "Tensor(c!) dv, int heads, float scale, Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, "
-        "float dropout_p, Tensor? seed, int salt, bool accumulate_dq, bool accumulate_dkv) -> ()");
+        "float dropout_p, Tensor? seed, int salt, bool accumulate_dq, bool accumulate_dkv, "
+        "Tensor(d!)? dqkv_planes=None, bool planes_only=False)-> ()");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, Tensor(a!) y, Tensor(b!) mean, "
         "Tensor(c!) rstd) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor? dx_add, "

@@ -201,11 +201,16 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         ctx.lin_grads([p + ".attention.output.dense"], g1, Bk.as2d(o), g1p, op)
         do = Bk.linear_dx(ctx, g1, p + ".attention.output.dense", dyp=g1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
+        # the packed gradient feeds only the QKV dX / dW GEMMs: planes straight from the attention
+        # backward, and no fp32 copy when both run on split operands
+        T_ = B * L
+        dq2p, dq_out = Bk.out_planes(ctx, T_, 3 * D, [(3 * D, D, T_, True, True), (T_, D, 3 * D, False, True)],
+                                     dqkv.device)
         K.attn_bwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], o, lse, do, H, key_bias=st["kb"],
-                   dq=dqkv[..., :D], dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:], **attn_drop)
+                   dq=dqkv[..., :D], dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:], dqkv_planes=dq2p,
+                   planes_only=not dq_out, **attn_drop)
         names = [p + ".attention.self.query", p + ".attention.self.key", p + ".attention.self.value"]
         dq2 = Bk.as2d(dqkv)
-        dq2p = ctx.planes(dq2)
         ctx.lin_grads(names, dq2, x, dq2p, xp)
         Wp, _ = ctx.w_packed(names)
         dx = Bk.linear_dx(ctx, dq2, Wp, residual=ds1, dyp=dq2p)  # dx_in = ds1 + dQKV [Wq;Wk;Wv] (fresh buffer)
@@ -383,11 +388,13 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
         ctx.lin_grads([p + ".attention.output.dense"], dx1, Bk.as2d(o), dx1p, op)
         do = Bk.linear_dx(ctx, dx1, p + ".attention.output.dense", dyp=dx1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
+        T_ = qkv.shape[0] * qkv.shape[1]  # planes of the packed gradient from the kernels (see BERT)
+        dq2p, dq_out = Bk.out_planes(ctx, T_, 3 * D, [(3 * D, D, T_, True, True), (T_, D, 3 * D, False, True)],
+                                     dqkv.device)
         K.attn_bwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], o, lse, do, H, dq=dqkv[..., :D],
-                   dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:])
+                   dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:], dqkv_planes=dq2p, planes_only=not dq_out)
         names = [p + ".attention.attention.query", p + ".attention.attention.key", p + ".attention.attention.value"]
         dq2 = Bk.as2d(dqkv)
-        dq2p = ctx.planes(dq2)
         ctx.lin_grads(names, dq2, h, dq2p, hp)
         Wp, _ = ctx.w_packed(names)
         dh = Bk.linear_dx(ctx, dq2, Wp, dyp=dq2p)

@@ -90,6 +90,7 @@ class AttnArgs(ctypes.Structure):
         ("rel_bias_mod", ctypes.c_int64),
         ("cos_logit_scale", ctypes.c_void_p),
         ("cos_max_log", ctypes.c_float),
+        ("dqkv_planes", ctypes.c_void_p), ("planes_only", ctypes.c_int),
     ]
 
 
@@ -561,7 +562,11 @@ def attn_fill_masked_rows(v, o, H, mask):
 
 
 def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None, key_bias=None, rel_bias=None,
-             dropout_p=0.0, seed=None, salt=0, accumulate_dq=False, accumulate_dkv=False):
+             dropout_p=0.0, seed=None, salt=0, accumulate_dq=False, accumulate_dkv=False, dqkv_planes=None,
+             planes_only=False):
+    """dq, dk, dv (views of one packed [B, L, 3*H*D] buffer when `dqkv_planes` is given: bf16
+    [3, B*L, 3*H*D] split planes of that buffer, written by the kernels; planes_only skips the
+    fp32 stores — for a gradient read only by split-operand GEMMs, see x6_ok)"""
     _require_cuda(q, k, v, o, lse, dout)
     B, Lq, HD = q.shape
     Lk = k.shape[1]
@@ -574,7 +579,8 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
     rb, rb_sb, rb_mod = _rel_bias_args(rel_bias, B, H, Lq, Lk)
     _ops().attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, int(H), float(scale if scale is not None else D ** -0.5),
                     key_bias, rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
-                    seed.t if seed is not None else None, _salt(salt), bool(accumulate_dq), bool(accumulate_dkv))
+                    seed.t if seed is not None else None, _salt(salt), bool(accumulate_dq), bool(accumulate_dkv),
+                    dqkv_planes, bool(planes_only))
     return dq, dk, dv
 
 

@@ -546,3 +546,34 @@ def test_gemm_out_planes_equal_split_of_output(case):
         assert (recon - ref.double()).abs().max().item() <= 2 ** -23 * ref.abs().max().item()
     finally:
         K.set_fp32_gemm_mode(old)
+
+
+@pytest.mark.parametrize("L", [128, 197, 300])
+def test_attention_bwd_dqkv_planes(L):
+    """fp32 attention backward writing the split planes of the packed [dq | dk | dv] gradient: bit-
+    identical to split3 of the fp32 gradient (v2 kernels write them from their stores, L = 300 takes
+    the v1 kernels and a split pass); planes_only leaves the fp32 buffer untouched"""
+    B, H, D = 3, 4, 64
+    g = torch.Generator().manual_seed(L)
+    qkv = torch.randn(B, L, 3 * H * D, generator=g).to(DEV)
+    q, k, v = qkv[..., :H * D], qkv[..., H * D:2 * H * D], qkv[..., 2 * H * D:]
+    o, lse = K.attn_fwd(q, k, v, H)
+    do = torch.randn(B, L, H * D, generator=g).to(DEV)
+    dqkv = torch.empty_like(qkv)
+    K.attn_bwd(q, k, v, o, lse, do, H, dq=dqkv[..., :H * D], dk=dqkv[..., H * D:2 * H * D], dv=dqkv[..., 2 * H * D:])
+    pl = torch.empty((3, B * L, 3 * H * D), device=DEV, dtype=torch.bfloat16)
+    d2 = torch.empty_like(qkv)
+    K.attn_bwd(q, k, v, o, lse, do, H, dq=d2[..., :H * D], dk=d2[..., H * D:2 * H * D], dv=d2[..., 2 * H * D:],
+               dqkv_planes=pl)
+    torch.cuda.synchronize()
+    assert torch.equal(d2, dqkv)
+    ref = K.split3(dqkv.view(B * L, -1))
+    assert torch.equal(pl.view(torch.int16), ref.view(torch.int16))
+    d3 = torch.full_like(qkv, 5.0)
+    pl2 = torch.empty_like(pl)
+    K.attn_bwd(q, k, v, o, lse, do, H, dq=d3[..., :H * D], dk=d3[..., H * D:2 * H * D], dv=d3[..., 2 * H * D:],
+               dqkv_planes=pl2, planes_only=True)
+    torch.cuda.synchronize()
+    assert torch.equal(pl2.view(torch.int16), ref.view(torch.int16))
+    if L <= 256:
+        assert bool((d3 == 5.0).all())
