@@ -296,7 +296,14 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   const int wr = wave >> 2, wc = wave & 3;
   G8_STAMP(0);
   const int gx = gridDim.x, gy = gridDim.y;
-  const int tile = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  // XCD-aware order over the whole grid, split-K index included: the hardware deals workgroups
+  // round-robin over the 8 XCDs in linear (x, y, z) order, and each XCD gets a contiguous run of
+  // (split, row, column) tiles — the blocks of one K range sharing A / B panels sit in one L2
+  // (remapping (x, y) alone put split z's tiles on XCD (id + 36 z) mod 8: the split-K weight-
+  // gradient GEMMs re-fetched their operands 4-5x)
+  const int lt = xcd_remap((blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x, gx * gy * gridDim.z);
+  const int split = lt / (gx * gy);
+  const int tile = lt - split * (gx * gy);
   // grouped raster: an XCD's consecutive tiles sweep group_m row panels x the column tiles, so the
   // ~32 tiles it runs at once share group_m A panels and 32/group_m B panels in its L2
   int trow, tcol;
@@ -310,7 +317,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   constexpr int G8_BK = G8T<T>::BK;
   constexpr int64_t ESZ = sizeof(T);
   const int nkt_total = X6 ? 6 * x6.nkt : (int)((K + G8_BK - 1) / G8_BK);
-  const int kt0 = blockIdx.z * tiles_per_split;
+  const int kt0 = split * tiles_per_split;
   const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
 
   f32x4 acc[2][2][4][2];
@@ -470,7 +477,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     rs1 += __shfl_xor(rs1, 16, 64);
     rs1 += __shfl_xor(rs1, 32, 64);
     if (lane < 16) {
-      float* dst = rs_mode == 1 ? rs_out : rs_out + (int64_t)blockIdx.z * M;
+      float* dst = rs_mode == 1 ? rs_out : rs_out + (int64_t)split * M;
       const float bt = rs_mode == 1 ? rs_beta : 0.f;
       const int64_t r0 = m0 + wr * 64 + wc * 16 + lane, r1 = r0 + 128;
       if (r0 < M) dst[r0] = (bt != 0.f ? bt * dst[r0] : 0.f) + rs0;
@@ -484,7 +491,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
   const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
-  float* slab = ws ? ws + (int64_t)blockIdx.z * M * N : nullptr;
+  float* slab = ws ? ws + (int64_t)split * M * N : nullptr;
   // fast path (full tile, 16-B aligned operands, no split-K slab): every thread owns the same 8
   // columns in all its rows, so the bias is loaded once; per pass all residual / aux / C loads of
   // the thread's 8 rows are issued before any math or store (one wait per pass, not per row)
