@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-2 (split-operand fp32 GEMMs) profile set, run via gpurun from the repo root: the fp32
+# headline step with the encoders serialized (per-kernel figures that match the bench's GEMM probe):
+# kernel trace + FETCH_SIZE + WRITE_SIZE + MFMA counters; the step as benched (two streams, graph)
+# kernel trace only; the bf16 leg's kernel trace.
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+MMFD_SERIAL_ENCODERS=1 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh r02g_fp32
+MMFD_SERIAL_ENCODERS=1 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/pmc_mfma.sh r02g_fp32
+PMC=0 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh r02g_fp32_step
+MMFD_SERIAL_ENCODERS=1 PMC=0 STEPS=4 BENCH_ARGS="--precision bf16 --no-bf16" bash tools/profile.sh r02g_bf16
