@@ -383,10 +383,16 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   g8_barrier();
   if (wr == 1) g8_barrier();  // stagger the second wave row by one barrier
 
-  // fused row sums of op(A) (bias gradient): blocks of the first column tile only; wave wc sums
-  // A subtile i == wc of each A fragment set it loads, lane (g, i) covering k-chunk g of row i
-  const bool do_rs = rs_mode != 0 && tcol == 0;
+  // fused row sums of op(A) (bias gradient); wave wc sums A subtile i == wc of each A fragment set
+  // it loads, lane (g, i) covering k-chunk g of row i. rs_mode 1 / 2: the first column tile sums
+  // every K-tile (direct / per-split partials); rs_mode 3: the gx column tiles share the K-tiles
+  // round robin (K-tile v goes to column tile v mod gx) into per-(split, column tile) partials —
+  // one column of blocks doing all of it made the whole launch wait on them (+25 % on the
+  // weight-gradient GEMMs)
+  const int rs_cols = rs_mode == 3 ? gx : 1;
+  const bool do_rs = rs_mode != 0 && tcol < rs_cols;
   float rs0 = 0.f, rs1 = 0.f;
+  int rs_ph = (kt0 % rs_cols);  // column tile owning the current K-tile's row sums
   // X6: only the segments that carry each A plane once contribute to the row sums
   auto rs_on = [&](int t) { return !X6 || ((X6_RS >> ((kt0 + t) / x6.nkt)) & 1u); };
 
@@ -400,11 +406,16 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     // phase then waits until at most the 8 pieces issued after the next phase's operands remain.
     uint4 fbh[2][2];
     for (int t = 0; t < nk; ++t) {
+      bool rs_t = false;
+      if (do_rs) {  // (uniform; kept off the path of GEMMs without row sums)
+        rs_t = rs_ph == tcol && rs_on(t);
+        rs_ph = rs_ph + 1 == rs_cols ? 0 : rs_ph + 1;
+      }
       // phase X(t)
       g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
       g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
       g8_frag_b<T, TB>(fbh, img(t, 3), wc, lane);
-      if (do_rs && rs_on(t)) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (rs_t) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
       if (t + 1 < nk) {
         issue(1, t + 1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -416,7 +427,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_barrier();
       // phase Y(t)
       g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
-      if (do_rs && rs_on(t)) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (rs_t) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
       if (t + 2 < nk) {
         issue(0, t + 2); issue(2, t + 2); issue(3, t + 2);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -431,10 +442,15 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     // fp32: four phases of one quadrant each (the two-phase schedule pushes the fp32 layout-1
     // fragment addressing past 256 VGPRs into scratch and measured no faster)
     for (int t = 0; t < nk; ++t) {
+      bool rs_t = false;
+      if (do_rs) {
+        rs_t = rs_ph == tcol;
+        rs_ph = rs_ph + 1 == rs_cols ? 0 : rs_ph + 1;
+      }
       // phase 0: quadrant (0,0)
       g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
       g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
-      if (do_rs) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (rs_t) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
       if (t + 1 < nk) issue(2, t + 1);
       g8_pre_barrier();
       g8_mma<T>(acc[0][0], fa, fb);
@@ -447,7 +463,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_barrier();
       // phase 2: quadrant (1,1)
       g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
-      if (do_rs) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (rs_t) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
       if (t + 2 < nk) issue(3, t + 2);
       g8_pre_barrier();
       g8_mma<T>(acc[1][1], fa, fb);
@@ -477,7 +493,7 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     rs1 += __shfl_xor(rs1, 16, 64);
     rs1 += __shfl_xor(rs1, 32, 64);
     if (lane < 16) {
-      float* dst = rs_mode == 1 ? rs_out : rs_out + (int64_t)split * M;
+      float* dst = rs_mode == 1 ? rs_out : rs_out + (int64_t)(split * rs_cols + tcol) * M;
       const float bt = rs_mode == 1 ? rs_beta : 0.f;
       const int64_t r0 = m0 + wr * 64 + wc * 16 + lane, r1 = r0 + 128;
       if (r0 < M) dst[r0] = (bt != 0.f ? bt * dst[r0] : 0.f) + rs0;
@@ -742,13 +758,14 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
                                      int64_t ldc, int64_t M, int64_t N, EpiArgs e, const float* __restrict__ rs_part,
+                                     int rs_nparts,
                                      float* __restrict__ rs_out, float rs_beta) {
   const uint32_t seed = (e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
   const int64_t total = M * N;
   if (rs_part) {  // the fused row sums' per-split partials (G8 split-K), summed in split order
     for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
       float t = 0.f;
-      for (int s = 0; s < splits; ++s) t += rs_part[(int64_t)s * M + m];
+      for (int s = 0; s < rs_nparts; ++s) t += rs_part[(int64_t)s * M + m];
       rs_out[m] = (rs_beta != 0.f ? rs_beta * rs_out[m] : 0.f) + t;
     }
   }
@@ -993,7 +1010,10 @@ int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 // extra workspace for the fused row sums: per-split partials (G8) or the colsum partials (others)
 int64_t rowsum_ws_bytes(const mmfd_gemm_args& a, int splits, bool g8) {
   if (!a.a_rowsum) return 0;
-  if (g8) return splits > 1 ? (int64_t)splits * a.M * 4 : 0;
+  if (g8) {  // per-(split, column tile) partials (gemm256_kernel rs_mode 3)
+    const int64_t parts = (int64_t)splits * ((a.N + G8_BN - 1) / G8_BN);
+    return parts > 1 ? parts * a.M * 4 : 0;
+  }
   const int64_t nparts = std::min<int64_t>(256, std::max<int64_t>(1, a.K / 64));
   return nparts * a.M * 4;
 }
@@ -1115,9 +1135,17 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   float* ws = splits > 1 ? (float*)a.workspace : nullptr;
   const bool g8 = use_g8(a);
   // fused row sums: G8 writes them directly (one split) or as per-split partials after the slabs
-  float* rs_part = (a.a_rowsum && g8 && splits > 1) ? (float*)a.workspace + (int64_t)splits * a.M * a.N : nullptr;
-  const int rs_mode = (!a.a_rowsum || !g8) ? 0 : (splits > 1 ? 2 : 1);
-  float* rs_out = rs_mode == 2 ? rs_part : a.a_rowsum;
+  // row-sum partials after the split-K slabs: [splits][column tiles][M] when the workspace holds
+  // them (rs_mode 3), else the first column tile sums alone (per-split partials / direct)
+  const int64_t gxt = (a.N + G8_BN - 1) / G8_BN;
+  const int64_t slab_bytes = ws ? (int64_t)splits * a.M * a.N * 4 : 0;
+  const int rs_parts3 = (int)(splits * gxt);
+  const bool rs3 = a.a_rowsum && g8 && rs_parts3 > 1 && a.workspace &&
+                   a.workspace_bytes >= slab_bytes + (int64_t)rs_parts3 * a.M * 4;
+  float* rs_part = (a.a_rowsum && g8 && (rs3 || splits > 1)) ? (float*)((char*)a.workspace + slab_bytes) : nullptr;
+  const int rs_mode = (!a.a_rowsum || !g8) ? 0 : (rs3 ? 3 : (splits > 1 ? 2 : 1));
+  const int rs_nparts = rs_mode == 3 ? rs_parts3 : splits;
+  float* rs_out = rs_mode >= 2 ? rs_part : a.a_rowsum;
 
   if (xp.on) {
     char* planes = (char*)a.workspace + align256((int64_t)(splits > 1 ? splits : 0) * a.M * a.N * 4 +
@@ -1144,13 +1172,17 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   if (ws) {
     const int64_t total = a.M * a.N;
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-    // the row sums' split partials (rs_mode 2) are reduced by the same launch
-    const float* rsp = rs_mode == 2 ? rs_part : nullptr;
+    // the row sums' partials (rs_mode 2 / 3) are reduced by the same launch
+    const float* rsp = rs_mode >= 2 ? rs_part : nullptr;
     if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc,
-                                a.M, a.N, e, rsp, a.a_rowsum, a.a_rowsum_beta);
+                                a.M, a.N, e, rsp, rs_nparts, a.a_rowsum, a.a_rowsum_beta);
     else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc,
-                            a.M, a.N, e, rsp, a.a_rowsum, a.a_rowsum_beta);
+                            a.M, a.N, e, rsp, rs_nparts, a.a_rowsum, a.a_rowsum_beta);
     MMFD_CHECK_LAUNCH("splitk_reduce");
+  } else if (rs_mode == 3) {  // no split-K: only the column tiles' row-sum partials to reduce
+    hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((a.M + 63) / 64)), dim3(1024), 0, s,
+                       (const float*)rs_part, rs_nparts, a.M, a.M, a.a_rowsum, a.a_rowsum_beta);
+    MMFD_CHECK_LAUNCH("rowsum_reduce");
   }
   if (a.a_rowsum && !g8) {
     char* base = (char*)a.workspace + (ws ? (int64_t)splits * a.M * a.N * 4 : 0);
