@@ -876,11 +876,16 @@ void dispatch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
 // thread (two 16-B loads, one 16-B store per plane), cols % 8 == 0
 __global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ X, int64_t ldx, int64_t rows,
                                                      int64_t cols, bf16* __restrict__ P, int64_t plane) {
-  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c >= cols) return;
-  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
-    const float4 x0 = *reinterpret_cast<const float4*>(X + r * ldx + c);
-    const float4 x1 = *reinterpret_cast<const float4*>(X + r * ldx + c + 4);
+  // one 8-column chunk of one row per thread, grid-stride over all chunks (narrow rows — 768
+  // columns = 96 chunks — keep every lane busy)
+  const uint32_t c8 = (uint32_t)(cols / 8);
+  const uint32_t total = (uint32_t)(rows * c8);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t r = i / c8;
+    const int64_t c = (int64_t)(i - r * c8) * 8;
+    const float* src = X + (int64_t)r * ldx + c;
+    const float4 x0 = *reinterpret_cast<const float4*>(src);
+    const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
     const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
     bf16x8 h, m, l;
 #pragma unroll
@@ -892,7 +897,7 @@ __global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ X
       m[u] = mu;
       l[u] = (bf16)(r1 - (float)mu);
     }
-    bf16* d = P + r * cols + c;
+    bf16* d = P + (int64_t)r * cols + c;
     *reinterpret_cast<uint4*>(d) = __builtin_bit_cast(uint4, h);
     *reinterpret_cast<uint4*>(d + plane) = __builtin_bit_cast(uint4, m);
     *reinterpret_cast<uint4*>(d + 2 * plane) = __builtin_bit_cast(uint4, l);
@@ -900,9 +905,9 @@ __global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ X
 }
 
 void launch_split3(const float* X, int64_t ldx, int64_t rows, int64_t cols, bf16* P, hipStream_t s) {
-  const unsigned gx = (unsigned)((cols + 2047) / 2048);
-  const unsigned gy = (unsigned)std::min<int64_t>(rows, std::max<int64_t>(1, 16384 / gx));
-  hipLaunchKernelGGL(split3_kernel, dim3(gx, gy), dim3(256), 0, s, X, ldx, rows, cols, P, rows * cols);
+  const int64_t chunks = rows * (cols / 8);
+  const unsigned blocks = (unsigned)std::min<int64_t>((chunks + 255) / 256, 8192);
+  hipLaunchKernelGGL(split3_kernel, dim3(blocks), dim3(256), 0, s, X, ldx, rows, cols, P, rows * cols);
 }
 
 // fp32 x fp32 -> fp32 GEMM mode: 1 = split operands (six bf16 MFMA products per fp32 product, see
@@ -1196,6 +1201,7 @@ extern "C" int mmfd_split3(int64_t rows, int64_t cols, const float* x, int64_t l
   MMFD_CHECK_ARG(rows >= 0 && cols >= 0 && ld >= cols, "mmfd_split3: bad shape");
   MMFD_CHECK_ARG(cols % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)planes & 15) == 0,
                  "mmfd_split3: cols must be a multiple of 8 and rows 16-B aligned");
+  MMFD_CHECK_ARG(rows * (cols / 8) < (1ll << 32) && rows * ld < (1ll << 31), "mmfd_split3: matrix too large");
   if (rows == 0 || cols == 0) return 0;
   launch_split3(x, ld, rows, cols, (bf16*)planes, (hipStream_t)stream);
   MMFD_CHECK_LAUNCH("split3");
