@@ -6,7 +6,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-MMFD_SERIAL_ENCODERS=1 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh r02g_fp32
-MMFD_SERIAL_ENCODERS=1 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/pmc_mfma.sh r02g_fp32
-PMC=0 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh r02g_fp32_step
-MMFD_SERIAL_ENCODERS=1 PMC=0 STEPS=4 BENCH_ARGS="--precision bf16 --no-bf16" bash tools/profile.sh r02g_bf16
+MMFD_SERIAL_ENCODERS=1 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh ${TAG:-r02g}_fp32
+MMFD_SERIAL_ENCODERS=1 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/pmc_mfma.sh ${TAG:-r02g}_fp32
+PMC=0 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh ${TAG:-r02g}_fp32_step
+MMFD_SERIAL_ENCODERS=1 PMC=0 STEPS=4 BENCH_ARGS="--precision bf16 --no-bf16" bash tools/profile.sh ${TAG:-r02g}_bf16
