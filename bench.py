@@ -728,9 +728,13 @@ def train_leg(args, dev, world, rank, precision):
     # step they overlap on two streams, which is faster overall but stretches each kernel's
     # duration by the CUs the other stream holds — the roofline is a property of the kernel alone
     steps_in_prof = 2
+    conc, tr.concurrent = tr.concurrent, False
     if graphed:  # the graph's private pool would double the eager probe's footprint
         tr.release_graph()
-    conc, tr.concurrent = tr.concurrent, False
+    # one untimed eager step first: it refills the caching allocator (the hipMallocs of a cold pool
+    # would otherwise sit between the probe's events and inflate the first step's GEMM times)
+    tr.step(batch)
+    torch.cuda.synchronize()
     with probe:
         for _ in range(steps_in_prof):
             tr.step(batch)

@@ -97,6 +97,7 @@ class StepCtx:
         self.side = None         # stream for weight-gradient GEMMs (enable_side_stream)
         self.cache_derived = False  # keep weight-derived tensors across calls (see derived())
         self._side_used = False
+        self._wp = {}            # split planes of fp32 weights, by data_ptr (one split per call)
 
     def enable_side_stream(self, device):
         self.side = side_stream(device)
@@ -212,6 +213,17 @@ class StepCtx:
         self.shadows[("derived", key)] = (sig, t)
         return t
 
+    def wplanes(self, W):
+        """split planes of an fp32 weight matrix, made once per forward/backward of the module and
+        shared by its forward and data-gradient GEMMs (None outside split-operand fp32 mode)"""
+        if self.dt != torch.float32 or not K.split_eligible(W):
+            return None
+        key = (W.data_ptr(), tuple(W.shape), W.stride(0))
+        p = self._wp.get(key)
+        if p is None:
+            p = self._wp[key] = K.split3(W)
+        return p
+
     def planes(self, t):
         """bf16 planes of an fp32 GEMM operand (kernels.split3) when the fp32 GEMMs run on split
         operands, else None: split once, read by every GEMM that takes `t` (the forward input
@@ -312,7 +324,8 @@ def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=
     if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
         aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
     y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,
-               a_planes=xp, out_planes=out_planes, write_out=write_out, **(ctx.drop(drop_site) if drop_site else {}))
+               a_planes=xp, b_planes=ctx.wplanes(W) if xp is not None else None, out_planes=out_planes,
+               write_out=write_out, **(ctx.drop(drop_site) if drop_site else {}))
     return y, aux
 
 
@@ -329,14 +342,15 @@ def out_planes(ctx: StepCtx, rows, cols, consumers, device):
 
 def linear_packed(ctx: StepCtx, x2d, names, xp=None):
     W, b = ctx.w_packed(names)
-    return K.gemm(x2d, W, bias=b, a_planes=xp)
+    return K.gemm(x2d, W, bias=b, a_planes=xp, b_planes=ctx.wplanes(W) if xp is not None else None)
 
 
 def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
               residual=None, dyp=None, out_planes=None, write_out=True):
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
     return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
-                  residual=residual, a_planes=dyp, out_planes=out_planes, write_out=write_out,
+                  residual=residual, a_planes=dyp, b_planes=ctx.wplanes(W) if dyp is not None else None,
+                  out_planes=out_planes, write_out=write_out,
                   **(ctx.drop(drop_site) if drop_site else {}))
 
 

@@ -4,7 +4,7 @@ import torch
 import mmfd
 from mmfd.train import build_flagship
 from mmfd.dataset import synthetic_batch
-tr = build_flagship("cuda", "bf16")
+tr = build_flagship("cuda", sys.argv[1] if len(sys.argv) > 1 else "bf16")
 b = synthetic_batch(8, device="cuda")
 tr.step(b); tr.step(b); torch.cuda.synchronize()
 from torch.profiler import profile, ProfilerActivity
