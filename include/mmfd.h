@@ -98,6 +98,9 @@ typedef struct mmfd_gemm_args {
      weight-gradient GEMMs — reads them instead of splitting again. NULL = split here. Ignored by
      the other paths. */
   const void* a_planes; const void* b_planes;
+  /* 1: the fp32 A / B was never written (its only form is the planes): mmfd_gemm fails with
+     MMFD_ERR_UNSUPPORTED instead of reading it when the split-operand path is not taken */
+  int a_planes_only, b_planes_only;
 } mmfd_gemm_args;
 
 int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);

@@ -305,8 +305,10 @@ class StepCtx:
         for n in names:
             rows = self.P[n + ".weight"].shape[0]
             # (a planes-only gradient has no fp32 copy to slice: slice its planes instead)
-            self._lin_grads([n], dy2d[:, r:r + rows], x2d,
-                            dyp[:, :, r:r + rows].contiguous() if dyp is not None else None, xp)
+            dys = dy2d[:, r:r + rows]
+            if getattr(dy2d, "_mmfd_planes_only", False):
+                dys._mmfd_planes_only = True
+            self._lin_grads([n], dys, x2d, dyp[:, :, r:r + rows].contiguous() if dyp is not None else None, xp)
             r += rows
 
 

@@ -1124,6 +1124,10 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     const int64_t wneed = mmfd_gemm_workspace_bytes(&a);
     if (wneed > 0 && (a.workspace == nullptr || a.workspace_bytes < wneed)) xp.on = false;
   }
+  if (!xp.on && (a.a_planes_only || a.b_planes_only))
+    return mmfd_set_error(MMFD_ERR_UNSUPPORTED, "mmfd_gemm: an operand exists only as split planes, but this "
+                          "product (M %lld N %lld K %lld) does not run on split operands", (long long)a.M,
+                          (long long)a.N, (long long)a.K);
   int64_t need = 0;
   int splits = choose_splits(a, &need, xp.on);
   if (!xp.on && splits > 1 && (a.workspace == nullptr || a.workspace_bytes < need + rowsum_ws_bytes(a, splits, use_g8(a)))) {

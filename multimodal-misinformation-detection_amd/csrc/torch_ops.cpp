@@ -54,7 +54,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
           const std::optional<at::Tensor>& seed, int64_t salt, int64_t splits, const std::optional<at::Tensor>& a_rowsum,
           double a_rowsum_beta, const std::optional<at::Tensor>& a_planes = std::nullopt,
           const std::optional<at::Tensor>& b_planes = std::nullopt,
-          const std::optional<at::Tensor>& out_planes = std::nullopt, bool write_out = true) {
+          const std::optional<at::Tensor>& out_planes = std::nullopt, bool write_out = true,
+          bool a_planes_only = false, bool b_planes_only = false) {
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "mmfd::gemm operands must share a dtype");
   mmfd_gemm_args a{};
   a.dtype = dtype_code(A);
@@ -91,6 +92,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
   };
   a.a_planes = planes(a_planes, A, "a_planes");
   a.b_planes = planes(b_planes, B, "b_planes");
+  a.a_planes_only = (a_planes_only && a.a_planes) ? 1 : 0;
+  a.b_planes_only = (b_planes_only && a.b_planes) ? 1 : 0;
   if (out_planes.has_value() && out_planes->defined()) {
     TORCH_CHECK(out.scalar_type() == at::kFloat, "mmfd::gemm: out_planes need an fp32 output");
     a.ep.out_planes = const_cast<void*>(planes(out_planes, out, "out_planes"));
@@ -289,7 +292,7 @@ TORCH_LIBRARY(mmfd, m) {
   m.def("gemm(Tensor A, Tensor B, bool trans_a, bool trans_b, Tensor(a!) out, float alpha, float beta, Tensor? bias, "
         "Tensor? residual, bool residual_first, int act, Tensor(b!)? aux, float dropout_p, Tensor? seed, int salt, "
         "int splits, Tensor(c!)? a_rowsum, float a_rowsum_beta, Tensor? a_planes=None, Tensor? b_planes=None, "
-        "Tensor(d!)? out_planes=None, bool write_out=True) -> ()");
+        "Tensor(d!)? out_planes=None, bool write_out=True, bool a_planes_only=False, bool b_planes_only=False) -> ()");
   m.def("split3(Tensor x, Tensor(a!) planes) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, int act=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) out, Tensor(b!) lse, int heads, float scale, "

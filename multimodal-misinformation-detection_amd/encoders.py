@@ -211,6 +211,7 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
                    planes_only=not dq_out, **attn_drop)
         names = [p + ".attention.self.query", p + ".attention.self.key", p + ".attention.self.value"]
         dq2 = Bk.as2d(dqkv)
+        dq2._mmfd_planes_only = not dq_out
         ctx.lin_grads(names, dq2, x, dq2p, xp)
         Wp, _ = ctx.w_packed(names)
         dx = Bk.linear_dx(ctx, dq2, Wp, residual=ds1, dyp=dq2p)  # dx_in = ds1 + dQKV [Wq;Wk;Wv] (fresh buffer)
@@ -395,6 +396,7 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
                    dk=dqkv[..., D:2 * D], dv=dqkv[..., 2 * D:], dqkv_planes=dq2p, planes_only=not dq_out)
         names = [p + ".attention.attention.query", p + ".attention.attention.key", p + ".attention.attention.value"]
         dq2 = Bk.as2d(dqkv)
+        dq2._mmfd_planes_only = not dq_out
         ctx.lin_grads(names, dq2, h, dq2p, hp)
         Wp, _ = ctx.w_packed(names)
         dh = Bk.linear_dx(ctx, dq2, Wp, dyp=dq2p)

@@ -61,6 +61,7 @@ class GemmArgs(ctypes.Structure):
         ("splits", ctypes.c_int),
         ("a_rowsum", ctypes.c_void_p), ("a_rowsum_beta", ctypes.c_float),
         ("a_planes", ctypes.c_void_p), ("b_planes", ctypes.c_void_p),
+        ("a_planes_only", ctypes.c_int), ("b_planes_only", ctypes.c_int),
     ]
 
 
@@ -402,7 +403,10 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
     _ops().gemm(A, B, bool(trans_a), bool(trans_b), out, float(alpha), float(beta), bias, residual,
                 bool(residual_first), int(act), aux, float(dropout_p), seed.t if seed is not None else None,
                 _salt(salt), int(splits), a_rowsum, float(a_rowsum_beta), a_planes, b_planes, out_planes,
-                bool(write_out))
+                bool(write_out), bool(getattr(A, "_mmfd_planes_only", False)),
+                bool(getattr(B, "_mmfd_planes_only", False)))
+    if not write_out:  # the fp32 output stays unwritten: only its planes may be read (checked in mmfd_gemm)
+        out._mmfd_planes_only = True
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()

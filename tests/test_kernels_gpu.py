@@ -577,3 +577,23 @@ def test_attention_bwd_dqkv_planes(L):
     assert torch.equal(pl2.view(torch.int16), ref.view(torch.int16))
     if L <= 256:
         assert bool((d3 == 5.0).all())
+
+
+def test_gemm_planes_only_operand_fails_loudly_off_the_split_path():
+    """an output written only as planes (write_out=False) is marked; a later GEMM that would read
+    its unwritten fp32 copy (here: fp32 MFMA mode) raises instead of computing on garbage"""
+    old = K.set_fp32_gemm_mode("split")
+    try:
+        x = _rand(512, 256, seed=71).to(DEV); w = _rand(384, 256, seed=72).to(DEV)
+        pl = torch.empty((3, 512, 384), device=DEV, dtype=torch.bfloat16)
+        y = K.gemm(x, w, out_planes=pl, write_out=False)
+        w2 = _rand(128, 384, seed=73).to(DEV)
+        ok = K.gemm(y, w2, a_planes=pl)  # split path: reads the planes
+        ref = (x.double() @ w.double().T) @ w2.double().T
+        torch.cuda.synchronize()
+        assert (ok.double() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+        K.set_fp32_gemm_mode("native")
+        with pytest.raises(RuntimeError, match="only as split planes"):
+            K.gemm(y, w2, a_planes=pl)
+    finally:
+        K.set_fp32_gemm_mode(old)
