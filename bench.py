@@ -659,6 +659,9 @@ def main():
             "step_mfma_frac": round(res["step_tflops"] / peak, 4),
             "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
             "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"],
+            "fp32_gemm": ("split operands: x = hi + mid + lo bf16 planes, six bf16 MFMA products accumulated in fp32 "
+                          "(error at the fp32 MFMA's level, tests/test_kernels_gpu.py; MMFD_FP32_GEMM=native selects "
+                          "the fp32 MFMA)" if K.fp32_gemm_mode() == 1 else "fp32 MFMA (v_mfma_f32_16x16x4f32)"),
         }
         if sec is not None:
             out["bf16"] = {"value": round(sec["pairs"], 2), "unit": "pairs/s", "ms_per_step": round(sec["ms"], 3),
