@@ -183,6 +183,12 @@ int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, in
 /* y = res + LN(x) (Swinv2's res-post-norm, modeling_swinv2.py Swinv2Layer.forward:
  * `shortcut + layernorm_before(attn)` and `h + layernorm_after(mlp)`); 16-B aligned rows;
  * mean/rstd may both be NULL (inference). */
+/* fp32 LayerNorm forward that also writes the output's bf16 split planes [3][rows][width]
+   (mmfd_split3 form, width % 8 == 0): the Linear inputs of the encoder layers, split in the same
+   pass (split-operand fp32 GEMMs, mmfd_set_fp32_gemm_mode) */
+int mmfd_layernorm_fwd_split(int64_t rows, int64_t width, const float* x, int64_t ldx, const float* gamma,
+                             const float* beta, float eps, float* y, int64_t ldy, float* mean, float* rstd,
+                             void* planes, mmfd_stream_t stream);
 int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
                            const float* gamma, const float* beta, float eps, const void* res, int64_t ldr,
                            void* y, int64_t ldy, float* mean, float* rstd, mmfd_stream_t stream);

@@ -363,6 +363,17 @@ def layernorm(ctx: StepCtx, x2d, name, eps):
     return K.layernorm_fwd(x2d, ctx.P[name + ".weight"], ctx.P[name + ".bias"], eps)
 
 
+def layernorm_planes(ctx: StepCtx, x2d, name, eps, want=True):
+    """(y, mean, rstd, planes): the LayerNorm output and, when `want` and the fp32 GEMMs run on split
+    operands, its split planes written by the same kernel (else None)"""
+    if want and ctx.dt == torch.float32 and x2d.shape[1] % 8 == 0 and K.split_eligible(x2d):
+        pl = torch.empty((3, x2d.shape[0], x2d.shape[1]), device=x2d.device, dtype=torch.bfloat16)
+        y, m, r = K.layernorm_fwd(x2d, ctx.P[name + ".weight"], ctx.P[name + ".bias"], eps, planes=pl)
+        return y, m, r, pl
+    y, m, r = layernorm(ctx, x2d, name, eps)
+    return y, m, r, None
+
+
 def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, drop_site=None):
     """Returns (dx, dx_dropped or None). Gamma/beta grads accumulate into ctx.grads."""
     gw, bw = ctx.grad_slot(name + ".weight", ctx.P[name + ".weight"].shape)

@@ -204,7 +204,8 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, 
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, T* __restrict__ y, int64_t ldy,
                                                        float* __restrict__ mean, float* __restrict__ rstd,
-                                                       const T* __restrict__ res = nullptr, int64_t ldr = 0) {
+                                                       const T* __restrict__ res = nullptr, int64_t ldr = 0,
+                                                       bf16* __restrict__ pl = nullptr, int64_t pl_stride = 0) {
   constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -247,6 +248,22 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, 
         for (int e = 0; e < N; ++e) o[e] += r[e];
       }
       VN<T>::store(y + row * ldy + N * c, o);
+      if constexpr (sizeof(T) == 4) {
+        if (pl) {  // fp32: the output's split planes (hi, mid, lo) for split-operand GEMMs
+          bf16 h[N], m[N], l[N];
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            h[e] = (bf16)o[e];
+            const float r1 = o[e] - (float)h[e];
+            m[e] = (bf16)r1;
+            l[e] = (bf16)(r1 - (float)m[e]);
+          }
+          bf16* d = pl + row * width + N * c;
+          *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, h);
+          *reinterpret_cast<uint2*>(d + pl_stride) = __builtin_bit_cast(uint2, m);
+          *reinterpret_cast<uint2*>(d + 2 * pl_stride) = __builtin_bit_cast(uint2, l);
+        }
+      }
     }
   }
   if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
@@ -519,6 +536,23 @@ extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const 
   else
     hipLaunchKernelGGL((ln_fwd_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
   MMFD_CHECK_LAUNCH("layernorm_fwd");
+  return 0;
+}
+
+extern "C" int mmfd_layernorm_fwd_split(int64_t rows, int64_t width, const float* x, int64_t ldx, const float* gamma,
+                                        const float* beta, float eps, float* y, int64_t ldy, float* mean, float* rstd,
+                                        void* planes, mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(width > 0 && width <= 1024 && width % 8 == 0, "layernorm_fwd_split: width %lld unsupported",
+                 (long long)width);
+  MMFD_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                     ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0 && ((uintptr_t)planes & 15) == 0,
+                 "layernorm_fwd_split: 16-B aligned rows required");
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, x, ldx, gamma, beta, eps, y,
+                     ldy, mean, rstd, (const float*)nullptr, (int64_t)0, (bf16*)planes, rows * width);
+  MMFD_CHECK_LAUNCH("layernorm_fwd_split");
   return 0;
 }
 

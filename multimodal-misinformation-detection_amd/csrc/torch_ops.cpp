@@ -202,7 +202,17 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
 
 // ---- LayerNorm ------------------------------------------------------------------------------------
 void layernorm_fwd(const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& beta, double eps, at::Tensor& y,
-                   at::Tensor& mean, at::Tensor& rstd) {
+                   at::Tensor& mean, at::Tensor& rstd, const std::optional<at::Tensor>& planes = std::nullopt) {
+  if (planes.has_value() && planes->defined()) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat && planes->scalar_type() == at::kBFloat16 && planes->is_contiguous() &&
+                    planes->numel() == 3 * x.size(0) * x.size(1),
+                "mmfd::layernorm_fwd: planes must be contiguous bf16 [3, rows, width] of an fp32 LayerNorm");
+    check(mmfd_layernorm_fwd_split(x.size(0), x.size(1), x.data_ptr<float>(), ld2(x, "x"), gamma.data_ptr<float>(),
+                                   beta.data_ptr<float>(), (float)eps, y.data_ptr<float>(), ld2(y, "y"),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), planes->data_ptr(), stream_of(x)),
+          "mmfd::layernorm_fwd");
+    return;
+  }
   check(mmfd_layernorm_fwd(dtype_code(x), x.size(0), x.size(1), x.data_ptr(), ld2(x, "x"), gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), (float)eps, y.data_ptr(), ld2(y, "y"), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), stream_of(x)), "mmfd::layernorm_fwd");
@@ -303,7 +313,7 @@ TORCH_LIBRARY(mmfd, m) {
         "float dropout_p, Tensor? seed, int salt, bool accumulate_dq, bool accumulate_dkv, "
         "Tensor(d!)? dqkv_planes=None, bool planes_only=False)-> ()");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, Tensor(a!) y, Tensor(b!) mean, "
-        "Tensor(c!) rstd) -> ()");
+        "Tensor(c!) rstd, Tensor(d!)? planes=None) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor? dx_add, "
         "Tensor(b!)? dgamma, Tensor(c!)? dbeta, float beta_acc, Tensor(d!)? dx_drop, float dropout_p, Tensor? seed, "
         "int salt) -> ()");

@@ -143,12 +143,13 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
                                    P["embeddings.LayerNorm.bias"], eps, ctx.dt, **emb_drop)
     kb = K.mask_to_bias(mask) if mask is not None else None
     states = []
+    xp = ctx.planes(x) if keep else None  # later layers: from the previous layer's LayerNorm
     for i in range(cfg.num_hidden_layers):
         p = f"encoder.layer.{i}"
         s = f"{site}.L{i}"
-        # split-operand fp32 GEMMs: every Linear input is split once here and the planes are kept
-        # for its weight-gradient GEMM (None in bf16 / fp32-MFMA mode)
-        xp = ctx.planes(x) if keep else None
+        # split-operand fp32 GEMMs: every Linear input is split once (by its producer: LayerNorm,
+        # GEMM epilogue, else split3) and the planes are kept for its weight-gradient GEMM (None in
+        # bf16 / fp32-MFMA mode)
         qkv = Bk.linear_packed(ctx, x, [p + ".attention.self.query", p + ".attention.self.key",
                                         p + ".attention.self.value"], xp=xp).view(B, L, 3 * D)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
@@ -157,8 +158,7 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
         op = ctx.planes(Bk.as2d(o)) if keep else None
         s1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, drop_site=s + ".attn_out",
                           xp=op)
-        h1, m1, r1 = Bk.layernorm(ctx, s1, p + ".attention.output.LayerNorm", eps)
-        h1p = ctx.planes(h1) if keep else None
+        h1, m1, r1, h1p = Bk.layernorm_planes(ctx, s1, p + ".attention.output.LayerNorm", eps, want=keep)
         T_, I_ = h1.shape[0], cfg.intermediate_size
         # the GELU output feeds only the FFN2 forward and FFN2 weight-gradient GEMMs: its planes come
         # from the FFN1 epilogue, and the fp32 copy is skipped when both run on split operands
@@ -167,10 +167,11 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
         f, pre = Bk.linear(ctx, h1, p + ".intermediate.dense", act=K.ACT_GELU, keep_aux=keep, xp=h1p,
                            out_planes=fp, write_out=f_out)
         s2, _ = Bk.linear(ctx, f, p + ".output.dense", residual=h1, drop_site=s + ".ffn_out", xp=fp)
-        x_out, m2, r2 = Bk.layernorm(ctx, s2, p + ".output.LayerNorm", eps)
+        x_out, m2, r2, xp_next = Bk.layernorm_planes(ctx, s2, p + ".output.LayerNorm", eps,
+                                                     want=keep and i + 1 < cfg.num_hidden_layers)
         if keep:
             states.append((x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop, (xp, op, h1p, fp)))
-        x = x_out
+        x, xp = x_out, xp_next
     st = dict(s0=s0, m0=m0, r0=r0, kb=kb, layers=states, emb_drop=emb_drop) if keep else None
     return x.view(B, L, D), st
 
@@ -347,15 +348,13 @@ def vit_forward(ctx: Bk.StepCtx, cfg: ViTConfig, px, keep):
     states = []
     for i in range(cfg.num_hidden_layers):
         p = f"encoder.layer.{i}"
-        h, mb, rb = Bk.layernorm(ctx, x, p + ".layernorm_before", eps)
-        hp = ctx.planes(h) if keep else None  # split once, kept for the weight-gradient GEMM (see BERT)
+        h, mb, rb, hp = Bk.layernorm_planes(ctx, x, p + ".layernorm_before", eps, want=keep)  # (see BERT)
         qkv = Bk.linear_packed(ctx, h, [p + ".attention.attention.query", p + ".attention.attention.key",
                                         p + ".attention.attention.value"], xp=hp).view(B, T, 3 * D)
         o, lse = K.attn_fwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], H)
         op = ctx.planes(Bk.as2d(o)) if keep else None
         x1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, xp=op)
-        h2, ma, ra = Bk.layernorm(ctx, x1, p + ".layernorm_after", eps)
-        h2p = ctx.planes(h2) if keep else None
+        h2, ma, ra, h2p = Bk.layernorm_planes(ctx, x1, p + ".layernorm_after", eps, want=keep)
         T_, I_ = h2.shape[0], cfg.intermediate_size
         fp, f_out = Bk.out_planes(ctx, T_, I_, [(T_, D, I_), (D, I_, T_, True, True)], h2.device) if keep \
             else (None, True)  # GELU output planes from the FFN1 epilogue (see BERT)

@@ -115,6 +115,7 @@ SIGNATURES = {
     "mmfd_set_fp32_gemm_mode": (_I, [_I]),
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
+    "mmfd_layernorm_fwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP, _VP]),
     "mmfd_colsum": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _F, _VP, _I64, _VP]),
     "mmfd_attn_fwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
     "mmfd_attn_bwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
@@ -591,13 +592,15 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
 # ------------------------------------------------------------------------------------------------
 # LayerNorm
 # ------------------------------------------------------------------------------------------------
-def layernorm_fwd(x2d, gamma, beta, eps, out=None):
+def layernorm_fwd(x2d, gamma, beta, eps, out=None, planes=None):
+    """y = LayerNorm(x); `planes` (bf16 [3, R, W], fp32 x only): the output's split3 planes, written
+    in the same pass"""
     _require_cuda(x2d, gamma, beta)
     R, W = x2d.shape
     y = out if out is not None else torch.empty((R, W), device=x2d.device, dtype=x2d.dtype)
     mean = torch.empty(R, device=x2d.device, dtype=torch.float32)
     rstd = torch.empty(R, device=x2d.device, dtype=torch.float32)
-    _ops().layernorm_fwd(x2d, gamma, beta, float(eps), y, mean, rstd)
+    _ops().layernorm_fwd(x2d, gamma, beta, float(eps), y, mean, rstd, planes)
     return y, mean, rstd
 
 

@@ -597,3 +597,18 @@ def test_gemm_planes_only_operand_fails_loudly_off_the_split_path():
             K.gemm(y, w2, a_planes=pl)
     finally:
         K.set_fp32_gemm_mode(old)
+
+
+@pytest.mark.parametrize("width", [64, 768])
+def test_layernorm_fwd_planes_equal_split_of_output(width):
+    """the fp32 LayerNorm forward writing its output's split planes in the same pass: y and the
+    statistics equal the plain kernel's, the planes equal split3(y) bit for bit"""
+    R = 1000
+    x = _rand(R, width, seed=81).to(DEV)
+    g = (1.0 + 0.1 * _rand(width, seed=82)).to(DEV); b = (0.1 * _rand(width, seed=83)).to(DEV)
+    y0, m0, r0 = K.layernorm_fwd(x, g, b, 1e-12)
+    pl = torch.empty((3, R, width), device=DEV, dtype=torch.bfloat16)
+    y1, m1, r1 = K.layernorm_fwd(x, g, b, 1e-12, planes=pl)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(m0, m1) and torch.equal(r0, r1)
+    assert torch.equal(pl.view(torch.int16), K.split3(y1).view(torch.int16))
