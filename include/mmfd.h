@@ -189,6 +189,14 @@ int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const void* x, in
 int mmfd_layernorm_fwd_split(int64_t rows, int64_t width, const float* x, int64_t ldx, const float* gamma,
                              const float* beta, float eps, float* y, int64_t ldy, float* mean, float* rstd,
                              void* planes, mmfd_stream_t stream);
+/* fp32 LayerNorm backward (as mmfd_layernorm_bwd) that also writes the bf16 split planes
+   [3][rows][width] of the gradient the next GEMMs read: dx_drop when given, else dx */
+int mmfd_layernorm_bwd_split(int64_t rows, int64_t width, const float* dy, int64_t lddy, const float* x,
+                             int64_t ldx, const float* gamma, const float* mean, const float* rstd,
+                             float* dx, int64_t lddx, const float* dx_add, int64_t ldadd, float* dgamma,
+                             float* dbeta, float beta_acc, float* dx_drop, float dropout_p,
+                             const uint64_t* seed, uint64_t salt, void* workspace,
+                             int64_t workspace_bytes, void* planes, mmfd_stream_t stream);
 int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, const void* x, int64_t ldx,
                            const float* gamma, const float* beta, float eps, const void* res, int64_t ldr,
                            void* y, int64_t ldy, float* mean, float* rstd, mmfd_stream_t stream);

@@ -363,10 +363,14 @@ def layernorm(ctx: StepCtx, x2d, name, eps):
     return K.layernorm_fwd(x2d, ctx.P[name + ".weight"], ctx.P[name + ".bias"], eps)
 
 
+# ablation switch: MMFD_NO_LN_PLANES=1 splits LayerNorm outputs in separate passes (split3) instead
+_NO_LN_PLANES = os.environ.get("MMFD_NO_LN_PLANES") == "1"
+
+
 def layernorm_planes(ctx: StepCtx, x2d, name, eps, want=True):
     """(y, mean, rstd, planes): the LayerNorm output and, when `want` and the fp32 GEMMs run on split
     operands, its split planes written by the same kernel (else None)"""
-    if want and ctx.dt == torch.float32 and x2d.shape[1] % 8 == 0 and K.split_eligible(x2d):
+    if want and ctx.dt == torch.float32 and x2d.shape[1] % 8 == 0 and K.split_eligible(x2d) and not _NO_LN_PLANES:
         pl = torch.empty((3, x2d.shape[0], x2d.shape[1]), device=x2d.device, dtype=torch.bfloat16)
         y, m, r = K.layernorm_fwd(x2d, ctx.P[name + ".weight"], ctx.P[name + ".bias"], eps, planes=pl)
         return y, m, r, pl
@@ -374,7 +378,20 @@ def layernorm_planes(ctx: StepCtx, x2d, name, eps, want=True):
     return y, m, r, None
 
 
-def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, drop_site=None):
+def layernorm_bwd_planes(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, drop_site=None):
+    """layernorm_bwd plus the split planes of the gradient the next GEMMs read (the dropped one when
+    there is dropout), written by the same kernel in split-operand fp32 mode (else None):
+    (dx, dx_dropped or None, planes or None)"""
+    W = dy2d.shape[1]
+    if not (ctx.dt == torch.float32 and W % 8 == 0 and W // 4 > 32 and K.split_eligible(dy2d)) or _NO_LN_PLANES:
+        dx, dd = layernorm_bwd(ctx, dy2d, x2d, name, mean, rstd, dx_add=dx_add, drop_site=drop_site)
+        return dx, dd, None
+    pl = torch.empty((3, dy2d.shape[0], W), device=dy2d.device, dtype=torch.bfloat16)
+    dx, dd = layernorm_bwd(ctx, dy2d, x2d, name, mean, rstd, dx_add=dx_add, drop_site=drop_site, planes=pl)
+    return dx, dd, pl
+
+
+def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, drop_site=None, planes=None):
     """Returns (dx, dx_dropped or None). Gamma/beta grads accumulate into ctx.grads."""
     gw, bw = ctx.grad_slot(name + ".weight", ctx.P[name + ".weight"].shape)
     gb, bb = ctx.grad_slot(name + ".bias", ctx.P[name + ".bias"].shape)
@@ -385,7 +402,7 @@ def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, dro
         dd = torch.empty_like(dy2d)
         kw = dict(dx_drop=dd, dropout_p=ctx.p, seed=ctx.seed, salt=K.salt_of(drop_site))
     dx = K.layernorm_bwd(dy2d, x2d, ctx.P[name + ".weight"], mean, rstd, dx_add=dx_add, dgamma=gw, dbeta=gb,
-                         beta_acc=bw, **kw)
+                         beta_acc=bw, planes=planes, **kw)
     return dx, dd
 
 

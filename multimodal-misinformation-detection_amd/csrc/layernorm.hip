@@ -349,7 +349,8 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
                                                        T* __restrict__ dx, int64_t lddx, const T* __restrict__ dx_add,
                                                        int64_t ldadd, T* __restrict__ dx_drop, float p, uint32_t thr,
                                                        const uint64_t* __restrict__ seedp, uint64_t salt,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, bf16* __restrict__ pl = nullptr,
+                                                       int64_t pl_stride = 0) {
   constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
   __shared__ float red[4][2][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -403,6 +404,22 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
             o[e] = (p > 0.f && h < thr) ? 0.f : o[e] * (p > 0.f ? keep : 1.f);
           }
           VN<T>::store(dx_drop + row * lddx + N * c, o);
+        }
+        if constexpr (sizeof(T) == 4) {
+          if (pl) {  // fp32: split planes of the GEMM operand (dx_drop when present, else dx)
+            bf16 h[N], m[N], l[N];
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+              h[e] = (bf16)o[e];
+              const float r1 = o[e] - (float)h[e];
+              m[e] = (bf16)r1;
+              l[e] = (bf16)(r1 - (float)m[e]);
+            }
+            bf16* dpl = pl + row * width + N * c;
+            *reinterpret_cast<uint2*>(dpl) = __builtin_bit_cast(uint2, h);
+            *reinterpret_cast<uint2*>(dpl + pl_stride) = __builtin_bit_cast(uint2, m);
+            *reinterpret_cast<uint2*>(dpl + 2 * pl_stride) = __builtin_bit_cast(uint2, l);
+          }
         }
       }
     }
@@ -584,12 +601,49 @@ extern "C" int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, co
   return 0;
 }
 
+namespace {
+int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
+                       const void* x, int64_t ldx, const float* gamma, const float* mean,
+                       const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
+                       float* dgamma, float* dbeta, float beta_acc, void* dx_drop,
+                       float dropout_p, const uint64_t* seed, uint64_t salt,
+                       void* workspace, int64_t workspace_bytes, mmfd_stream_t stream, bf16* planes);
+}  // namespace
+
 extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
                                   const void* x, int64_t ldx, const float* gamma, const float* mean,
                                   const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
                                   float* dgamma, float* dbeta, float beta_acc, void* dx_drop,
                                   float dropout_p, const uint64_t* seed, uint64_t salt,
                                   void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
+  return layernorm_bwd_impl(dtype, rows, width, dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, dx_add, ldadd, dgamma,
+                            dbeta, beta_acc, dx_drop, dropout_p, seed, salt, workspace, workspace_bytes, stream,
+                            nullptr);
+}
+
+extern "C" int mmfd_layernorm_bwd_split(int64_t rows, int64_t width, const float* dy, int64_t lddy, const float* x,
+                                        int64_t ldx, const float* gamma, const float* mean, const float* rstd,
+                                        float* dx, int64_t lddx, const float* dx_add, int64_t ldadd, float* dgamma,
+                                        float* dbeta, float beta_acc, float* dx_drop, float dropout_p,
+                                        const uint64_t* seed, uint64_t salt, void* workspace,
+                                        int64_t workspace_bytes, void* planes, mmfd_stream_t stream) {
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  MMFD_CHECK_ARG(width % 8 == 0 && width / 4 > 32 && width <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
+                     lddx % 4 == 0 && (!dx_add || (ldadd % 4 == 0 && al(dx_add))) && al(dy) && al(x) && al(dx) &&
+                     al(gamma) && (!dx_drop || al(dx_drop)) && al(planes),
+                 "layernorm_bwd_split: fp32 rows of 132..1024 (multiple of 8) elements, 16-B aligned");
+  return layernorm_bwd_impl(MMFD_F32, rows, width, dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, dx_add, ldadd,
+                            dgamma, dbeta, beta_acc, dx_drop, dropout_p, seed, salt, workspace, workspace_bytes, stream,
+                            (bf16*)planes);
+}
+
+namespace {
+int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
+                       const void* x, int64_t ldx, const float* gamma, const float* mean,
+                       const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
+                       float* dgamma, float* dbeta, float beta_acc, void* dx_drop,
+                       float dropout_p, const uint64_t* seed, uint64_t salt,
+                       void* workspace, int64_t workspace_bytes, mmfd_stream_t stream, bf16* planes) {
   MMFD_CHECK_ARG(width > 0 && width <= 1024 && width % 4 == 0, "layernorm_bwd: width %lld unsupported", (long long)width);
   MMFD_CHECK_ARG(!(dx_drop && dropout_p > 0.f) || seed, "layernorm_bwd: dropout needs seed");
   if (rows == 0) return 0;
@@ -628,7 +682,7 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
     else
       hipLaunchKernelGGL((ln_bwd16_kernel<float>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const float*)dy,
                          lddy, (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx, (const float*)dx_add, ldadd,
-                         (float*)dx_drop, p, thr, seed, salt, (float*)workspace);
+                         (float*)dx_drop, p, thr, seed, salt, (float*)workspace, planes, rows * width);
   } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
                        (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd, (bf16*)dx_drop,
@@ -647,3 +701,4 @@ extern "C" int mmfd_layernorm_bwd(int dtype, int64_t rows, int64_t width, const 
   MMFD_CHECK_LAUNCH("layernorm_bwd");
   return 0;
 }
+}  // namespace

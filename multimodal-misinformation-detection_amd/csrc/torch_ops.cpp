@@ -222,11 +222,25 @@ void layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& 
                    const at::Tensor& rstd, at::Tensor& dx, const std::optional<at::Tensor>& dx_add,
                    const std::optional<at::Tensor>& dgamma, const std::optional<at::Tensor>& dbeta, double beta_acc,
                    const std::optional<at::Tensor>& dx_drop, double dropout_p, const std::optional<at::Tensor>& seed,
-                   int64_t salt) {
+                   int64_t salt, const std::optional<at::Tensor>& planes = std::nullopt) {
   const int64_t R = dy.size(0), W = dy.size(1);
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((R + 3) / 4, 2048));
   at::Tensor ws = at::empty({nb * 2 * W}, dy.options().dtype(at::kFloat));
   const bool has_add = dx_add.has_value() && dx_add->defined();
+  if (planes.has_value() && planes->defined()) {
+    TORCH_CHECK(dy.scalar_type() == at::kFloat && planes->scalar_type() == at::kBFloat16 && planes->is_contiguous() &&
+                    planes->numel() == 3 * R * W,
+                "mmfd::layernorm_bwd: planes must be contiguous bf16 [3, rows, width] of an fp32 LayerNorm");
+    check(mmfd_layernorm_bwd_split(R, W, dy.data_ptr<float>(), ld2(dy, "dy"), x.data_ptr<float>(), ld2(x, "x"),
+                                   gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                   dx.data_ptr<float>(), ld2(dx, "dx"), has_add ? dx_add->data_ptr<float>() : nullptr,
+                                   has_add ? ld2(*dx_add, "dx_add") : 0, ptr_or_null<float>(dgamma),
+                                   ptr_or_null<float>(dbeta), (float)beta_acc, ptr_or_null<float>(dx_drop),
+                                   (float)dropout_p, seed_ptr(seed), (uint64_t)salt, ws.data_ptr(), ws.numel() * 4,
+                                   planes->data_ptr(), stream_of(dy)),
+          "mmfd::layernorm_bwd");
+    return;
+  }
   check(mmfd_layernorm_bwd(dtype_code(dy), R, W, dy.data_ptr(), ld2(dy, "dy"), x.data_ptr(), ld2(x, "x"),
                            gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
                            ld2(dx, "dx"), has_add ? dx_add->data_ptr() : nullptr, has_add ? ld2(*dx_add, "dx_add") : 0,
@@ -316,7 +330,7 @@ TORCH_LIBRARY(mmfd, m) {
         "Tensor(c!) rstd, Tensor(d!)? planes=None) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor? dx_add, "
         "Tensor(b!)? dgamma, Tensor(c!)? dbeta, float beta_acc, Tensor(d!)? dx_drop, float dropout_p, Tensor? seed, "
-        "int salt) -> ()");
+        "int salt, Tensor(e!)? planes=None) -> ()");
   m.def("xent(Tensor[] logits, int[] cols, Tensor labels, Tensor(a!) loss, Tensor(b!)[] dlogits, "
         "Tensor? dloss_scale) -> ()");
   m.def("adamw(Tensor table, int n, int max_numel, float lr, float beta1, float beta2, float eps, "

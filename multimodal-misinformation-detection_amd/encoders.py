@@ -184,9 +184,8 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         p = f"encoder.layer.{i}"
         s = f"{site}.L{i}"
         x, qkv, o, lse, s1, m1, r1, h1, pre, f, s2, m2, r2, attn_drop, (xp, op, h1p, fp) = st["layers"][i]
-        ds2, ds2d = Bk.layernorm_bwd(ctx, dx, s2, p + ".output.LayerNorm", m2, r2, drop_site=s + ".ffn_out")
+        ds2, ds2d, g2p = Bk.layernorm_bwd_planes(ctx, dx, s2, p + ".output.LayerNorm", m2, r2, drop_site=s + ".ffn_out")
         g2 = ds2d if ds2d is not None else ds2
-        g2p = ctx.planes(g2)
         ctx.lin_grads([p + ".output.dense"], g2, f, g2p, fp)
         T_, I_ = g2.shape[0], cfg.intermediate_size
         dprep, dpre_out = Bk.out_planes(ctx, T_, I_, [(I_, D, T_, True, True), (T_, D, I_, False, True)], g2.device)
@@ -196,9 +195,9 @@ def bert_backward(ctx: Bk.StepCtx, cfg: BertConfig, dout, st, ids, tts, site="be
         # dh1 = ds2 + dpre W (a fresh buffer: the weight-gradient GEMM on the side stream may still be
         # reading ds2)
         dh1 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", residual=ds2, dyp=dprep)
-        ds1, ds1d = Bk.layernorm_bwd(ctx, dh1, s1, p + ".attention.output.LayerNorm", m1, r1, drop_site=s + ".attn_out")
+        ds1, ds1d, g1p = Bk.layernorm_bwd_planes(ctx, dh1, s1, p + ".attention.output.LayerNorm", m1, r1,
+                                                 drop_site=s + ".attn_out")
         g1 = ds1d if ds1d is not None else ds1
-        g1p = ctx.planes(g1)
         ctx.lin_grads([p + ".attention.output.dense"], g1, Bk.as2d(o), g1p, op)
         do = Bk.linear_dx(ctx, g1, p + ".attention.output.dense", dyp=g1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
@@ -371,11 +370,13 @@ def vit_forward(ctx: Bk.StepCtx, cfg: ViTConfig, px, keep):
 
 def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
     D, H = cfg.hidden_size, cfg.num_attention_heads
-    dx, _ = Bk.layernorm_bwd(ctx, Bk.as2d(dout).contiguous(), st["x_last"], "layernorm", st["mf"], st["rf"])
+    dx, _, dxp = Bk.layernorm_bwd_planes(ctx, Bk.as2d(dout).contiguous(), st["x_last"], "layernorm", st["mf"],
+                                         st["rf"])
     for i in reversed(range(cfg.num_hidden_layers)):
         p = f"encoder.layer.{i}"
         x, h, mb, rb, qkv, o, lse, x1, h2, ma, ra, pre, f, (hp, op, h2p, fp) = st["layers"][i]
-        dxp = ctx.planes(dx)
+        if dxp is None:
+            dxp = ctx.planes(dx)
         ctx.lin_grads([p + ".output.dense"], dx, f, dxp, fp)
         T_, I_ = dx.shape[0], cfg.intermediate_size
         dprep, dpre_out = Bk.out_planes(ctx, T_, I_, [(I_, D, T_, True, True), (T_, D, I_, False, True)], dx.device)
@@ -383,8 +384,9 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
                             write_out=dpre_out)
         ctx.lin_grads([p + ".intermediate.dense"], dpre, h2, dprep, h2p)
         dh2 = Bk.linear_dx(ctx, dpre, p + ".intermediate.dense", dyp=dprep)
-        dx1, _ = Bk.layernorm_bwd(ctx, dh2, x1, p + ".layernorm_after", ma, ra, dx_add=dx)
-        dx1p = ctx.planes(dx1)
+        dx1, _, dx1p = Bk.layernorm_bwd_planes(ctx, dh2, x1, p + ".layernorm_after", ma, ra, dx_add=dx)
+        if dx1p is None:
+            dx1p = ctx.planes(dx1)
         ctx.lin_grads([p + ".attention.output.dense"], dx1, Bk.as2d(o), dx1p, op)
         do = Bk.linear_dx(ctx, dx1, p + ".attention.output.dense", dyp=dx1p).view(o.shape)
         dqkv = torch.empty_like(qkv)
@@ -399,7 +401,7 @@ def vit_backward(ctx: Bk.StepCtx, cfg: ViTConfig, dout, st):
         ctx.lin_grads(names, dq2, h, dq2p, hp)
         Wp, _ = ctx.w_packed(names)
         dh = Bk.linear_dx(ctx, dq2, Wp, dyp=dq2p)
-        dx, _ = Bk.layernorm_bwd(ctx, dh, x, p + ".layernorm_before", mb, rb, dx_add=dx1)
+        dx, _, dxp = Bk.layernorm_bwd_planes(ctx, dh, x, p + ".layernorm_before", mb, rb, dx_add=dx1)
         ctx.flush_ready()
     dpatch, dcls, dpos = K.vit_tokens_bwd(dx.view(st["B"], st["T"], D))
     ctx.grads["embeddings.cls_token"] = dcls.view(1, 1, D)

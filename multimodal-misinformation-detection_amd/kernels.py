@@ -116,6 +116,8 @@ SIGNATURES = {
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
     "mmfd_layernorm_fwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP, _VP]),
+    "mmfd_layernorm_bwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP,
+                                      _F, _VP, _F, _VP, _U64, _VP, _I64, _VP, _VP]),
     "mmfd_colsum": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _F, _VP, _I64, _VP]),
     "mmfd_attn_fwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
     "mmfd_attn_bwd": (_I, [ctypes.POINTER(AttnArgs), _VP]),
@@ -621,12 +623,14 @@ def layernorm_fwd_res(x2d, gamma, beta, eps, res, out=None, stats=False):
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, *, dx=None, dx_add=None, dgamma=None, dbeta=None, beta_acc=0.0,
-                  dx_drop=None, dropout_p=0.0, seed=None, salt=0):
+                  dx_drop=None, dropout_p=0.0, seed=None, salt=0, planes=None):
+    """`planes` (bf16 [3, R, W], fp32 only): split planes of the gradient the next GEMMs read —
+    dx_drop when given, else dx — written by the same kernel"""
     _require_cuda(dy, x, gamma, mean, rstd)
     R, W = dy.shape
     dx = dx if dx is not None else torch.empty((R, W), device=dy.device, dtype=dy.dtype)
     _ops().layernorm_bwd(dy, x, gamma, mean, rstd, dx, dx_add, dgamma, dbeta, float(beta_acc), dx_drop,
-                         float(dropout_p), seed.t if seed is not None else None, _salt(salt))
+                         float(dropout_p), seed.t if seed is not None else None, _salt(salt), planes)
     return dx
 
 

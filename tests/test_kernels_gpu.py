@@ -612,3 +612,28 @@ def test_layernorm_fwd_planes_equal_split_of_output(width):
     torch.cuda.synchronize()
     assert torch.equal(y0, y1) and torch.equal(m0, m1) and torch.equal(r0, r1)
     assert torch.equal(pl.view(torch.int16), K.split3(y1).view(torch.int16))
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_layernorm_bwd_planes_equal_split_of_gemm_operand(drop):
+    """the fp32 LayerNorm backward writing the split planes of the gradient the next GEMMs read
+    (dx_drop with dropout, else dx): outputs equal the plain kernel's, planes == split3 bit for bit"""
+    R, W = 1000, 768
+    x = _rand(R, W, seed=91).to(DEV); dy = _rand(R, W, seed=92).to(DEV); add = _rand(R, W, seed=93).to(DEV)
+    g = (1.0 + 0.1 * _rand(W, seed=94)).to(DEV); b = torch.zeros(W, device=DEV)
+    _, mean, rstd = K.layernorm_fwd(x, g, b, 1e-12)
+    seed = K.Seed(5)
+    kw = dict(dropout_p=0.1, seed=seed, salt=K.salt_of("lnb")) if drop else {}
+    outs = []
+    for planes in (None, torch.empty((3, R, W), device=DEV, dtype=torch.bfloat16)):
+        dd = torch.empty_like(dy) if drop else None
+        dgm, dbt = torch.empty(W, device=DEV), torch.empty(W, device=DEV)
+        dx = K.layernorm_bwd(dy, x, g, mean, rstd, dx_add=add, dgamma=dgm, dbeta=dbt, dx_drop=dd, planes=planes, **kw)
+        outs.append((dx, dd, dgm, dbt, planes))
+    torch.cuda.synchronize()
+    (dx0, dd0, g0, b0, _), (dx1, dd1, g1, b1, pl) = outs
+    assert torch.equal(dx0, dx1) and torch.equal(g0, g1) and torch.equal(b0, b1)
+    src = dd1 if drop else dx1
+    if drop:
+        assert torch.equal(dd0, dd1)
+    assert torch.equal(pl.view(torch.int16), K.split3(src).view(torch.int16))
