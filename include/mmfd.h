@@ -168,6 +168,10 @@ typedef struct mmfd_attn_args {
      [B, Lq, 3*H*D] buffer starting at dq (Lq == Lk) — written beside it, or instead of it with
      planes_only (no accumulate): the operand of the QKV data- and weight-gradient GEMMs */
   void* dqkv_planes; int planes_only;
+  /* forward, fp32 only: bf16 split planes [3][B*Lq][H*D] of the output o (o a contiguous
+     [B, Lq, H*D] buffer), written beside it — the operand of the output projection's forward and
+     weight-gradient GEMMs */
+  void* o_planes;
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);

@@ -331,6 +331,14 @@ def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=
     return y, aux
 
 
+def new_planes(ctx: StepCtx, rows, cols, device):
+    """an empty bf16 [3, rows, cols] planes buffer for a producer kernel to fill in split-operand fp32
+    mode, else None"""
+    if ctx.dt != torch.float32 or K.fp32_gemm_mode() != 1 or cols % 8 or 6 * rows * cols >= (1 << 31) - 4096:
+        return None
+    return torch.empty((3, rows, cols), device=device, dtype=torch.bfloat16)
+
+
 def out_planes(ctx: StepCtx, rows, cols, consumers, device):
     """(planes, write_out) for a GEMM output in split-operand fp32 mode: bf16 [3, rows, cols]
     written by the producing epilogue, and whether the fp32 output is needed at all — it is not

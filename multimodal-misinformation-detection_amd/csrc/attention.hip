@@ -782,7 +782,13 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
       if (q < p.Lq) {
 #pragma unroll
         for (int d = 0; d < C::DT; ++d)
-          if (d * 16 + li < p.D) ob[q * p.o_st + d * 16 + li] = from_f32<T>(o[d][r] * inv);
+          if (d * 16 + li < p.D) {
+            const float val = o[d][r] * inv;
+            ob[q * p.o_st + d * 16 + li] = from_f32<T>(val);
+            if constexpr (std::is_same<T, float>::value) {
+              if (p.pl) plane_put(p, reinterpret_cast<const float*>(ob) + q * p.o_st + d * 16 + li, val);
+            }
+          }
       }
     }
     if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = (m + log2f(lsum)) * LN2;
@@ -1218,11 +1224,20 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   const bool v2 = (p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !getenv("MMFD_ATTN_V1");
   MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && bf && a->rel_bias),
                  "attn_fwd: cosine attention needs bf16, the resident-K/V kernel (Lk <= 256) and a rel_bias");
+  p.pl = nullptr; p.pl_only = 0;
+  const int64_t W = a->H * a->D;
+  if (a->o_planes) {
+    MMFD_CHECK_ARG(!bf && a->o_st == W && a->o_sb == a->Lq * W && W % 8 == 0,
+                   "attn_fwd: o_planes need an fp32 output in one contiguous [B, Lq, H*D] buffer");
+    if (v2) { p.pl = (bf16*)a->o_planes; p.pl_stride = p.B * p.Lq * W; p.pl_base = (const float*)a->o; }
+  }
   if (v2 && bf) { if (a->D > 32) launch_fwd_v2<bf16, 64>(p, s); else launch_fwd_v2<bf16, 32>(p, s); }
   else if (v2) { if (a->D > 32) launch_fwd_v2<float, 64>(p, s); else launch_fwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_fwd");
+  if (a->o_planes && !v2)  // the streaming kernels write fp32 only: split afterwards
+    return mmfd_split3(p.B * p.Lq, W, (const float*)a->o, W, a->o_planes, stream);
   return 0;
 }
 

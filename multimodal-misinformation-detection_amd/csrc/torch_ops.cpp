@@ -163,13 +163,18 @@ void attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at:
               int64_t heads, double scale, const std::optional<at::Tensor>& key_bias,
               const std::optional<at::Tensor>& rel_bias, int64_t rel_bias_sb, int64_t rel_bias_mod, double dropout_p,
               const std::optional<at::Tensor>& seed, int64_t salt, const std::optional<at::Tensor>& cos_logit_scale,
-              double cos_max_log) {
+              double cos_max_log, const std::optional<at::Tensor>& o_planes = std::nullopt) {
   mmfd_attn_args a = attn_args(q, k, v, heads, scale, key_bias, rel_bias, rel_bias_sb, rel_bias_mod, dropout_p, seed, salt);
   const void* p;
   head_view(out, "out", &p, &a.o_sb, &a.o_st); a.o = const_cast<void*>(p);
   a.lse = lse.data_ptr<float>();
   a.cos_logit_scale = ptr_or_null<const float>(cos_logit_scale);
   a.cos_max_log = (float)cos_max_log;
+  if (o_planes.has_value() && o_planes->defined()) {
+    TORCH_CHECK(o_planes->scalar_type() == at::kBFloat16 && o_planes->is_contiguous() && o_planes->numel() == 3 * out.numel(),
+                "mmfd::attn_fwd: o_planes must be contiguous bf16 [3, B*L, H*D]");
+    a.o_planes = o_planes->data_ptr();
+  }
   check(mmfd_attn_fwd(&a, stream_of(q)), "mmfd::attn_fwd");
 }
 
@@ -321,7 +326,7 @@ TORCH_LIBRARY(mmfd, m) {
   m.def("linear(Tensor x, Tensor w, Tensor? bias, int act=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) out, Tensor(b!) lse, int heads, float scale, "
         "Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, float dropout_p, Tensor? seed, int salt, "
-        "Tensor? cos_logit_scale, float cos_max_log) -> ()");
+        "Tensor? cos_logit_scale, float cos_max_log, Tensor(c!)? o_planes=None) -> ()");
   m.def("attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dout, Tensor(a!) dq, Tensor(b!) dk, "
         "Tensor(c!) dv, int heads, float scale, Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, "
         "float dropout_p, Tensor? seed, int salt, bool accumulate_dq, bool accumulate_dkv, "

@@ -154,8 +154,9 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
                                         p + ".attention.self.value"], xp=xp).view(B, L, 3 * D)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         attn_drop = dict(ctx.drop(s + ".attn")) if cfg.attention_probs_dropout_prob > 0 else {}
-        o, lse = K.attn_fwd(q, k, v, H, key_bias=kb, **attn_drop)
-        op = ctx.planes(Bk.as2d(o)) if keep else None
+        # the output's planes from the attention kernel itself (fp32 split-operand mode)
+        op = Bk.new_planes(ctx, B * L, D, q.device) if keep else None
+        o, lse = K.attn_fwd(q, k, v, H, key_bias=kb, o_planes=op, **attn_drop)
         s1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, drop_site=s + ".attn_out",
                           xp=op)
         h1, m1, r1, h1p = Bk.layernorm_planes(ctx, s1, p + ".attention.output.LayerNorm", eps, want=keep)
@@ -350,8 +351,8 @@ def vit_forward(ctx: Bk.StepCtx, cfg: ViTConfig, px, keep):
         h, mb, rb, hp = Bk.layernorm_planes(ctx, x, p + ".layernorm_before", eps, want=keep)  # (see BERT)
         qkv = Bk.linear_packed(ctx, h, [p + ".attention.attention.query", p + ".attention.attention.key",
                                         p + ".attention.attention.value"], xp=hp).view(B, T, 3 * D)
-        o, lse = K.attn_fwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], H)
-        op = ctx.planes(Bk.as2d(o)) if keep else None
+        op = Bk.new_planes(ctx, B * T, D, qkv.device) if keep else None
+        o, lse = K.attn_fwd(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], H, o_planes=op)
         x1, _ = Bk.linear(ctx, Bk.as2d(o), p + ".attention.output.dense", residual=x, xp=op)
         h2, ma, ra, h2p = Bk.layernorm_planes(ctx, x1, p + ".layernorm_after", eps, want=keep)
         T_, I_ = h2.shape[0], cfg.intermediate_size

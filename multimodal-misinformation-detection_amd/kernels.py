@@ -92,6 +92,7 @@ class AttnArgs(ctypes.Structure):
         ("cos_logit_scale", ctypes.c_void_p),
         ("cos_max_log", ctypes.c_float),
         ("dqkv_planes", ctypes.c_void_p), ("planes_only", ctypes.c_int),
+        ("o_planes", ctypes.c_void_p),
     ]
 
 
@@ -497,7 +498,7 @@ def _head_view(t, H, D):
 
 
 def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, dropout_p=0.0, seed=None, salt=0,
-             cos_logit_scale=None, cos_max_log=0.0):
+             cos_logit_scale=None, cos_max_log=0.0, o_planes=None):
     """q: [B, Lq, H*D], k/v: [B, Lk, H*D] (views into fused QKV buffers are fine).
     cos_logit_scale (fp32 [H], bf16 only): Swinv2 cosine attention, q/k normalised in the kernel.
     Returns (o [B, Lq, H*D], lse [B, H, Lq] fp32)."""
@@ -514,7 +515,7 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
         raise ValueError("cos_logit_scale must be a contiguous fp32 tensor of H values")
     _ops().attn_fwd(q, k, v, out, lse, int(H), float(scale if scale is not None else D ** -0.5), key_bias,
                     rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
-                    seed.t if seed is not None else None, _salt(salt), cos_logit_scale, float(cos_max_log))
+                    seed.t if seed is not None else None, _salt(salt), cos_logit_scale, float(cos_max_log), o_planes)
     return out, lse
 
 

@@ -637,3 +637,19 @@ def test_layernorm_bwd_planes_equal_split_of_gemm_operand(drop):
     if drop:
         assert torch.equal(dd0, dd1)
     assert torch.equal(pl.view(torch.int16), K.split3(src).view(torch.int16))
+
+
+@pytest.mark.parametrize("L", [128, 197, 300])
+def test_attention_fwd_output_planes(L):
+    """fp32 attention forward writing its output's split planes (v2 kernels from their stores, the
+    L = 300 streaming path by a split pass): o unchanged, planes == split3(o) bit for bit"""
+    B, H, D = 2, 4, 64
+    g = torch.Generator().manual_seed(L + 7)
+    qkv = torch.randn(B, L, 3 * H * D, generator=g).to(DEV)
+    q, k, v = qkv[..., :H * D], qkv[..., H * D:2 * H * D], qkv[..., 2 * H * D:]
+    o0, l0 = K.attn_fwd(q, k, v, H)
+    pl = torch.empty((3, B * L, H * D), device=DEV, dtype=torch.bfloat16)
+    o1, l1 = K.attn_fwd(q, k, v, H, o_planes=pl)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
+    assert torch.equal(pl.view(torch.int16), K.split3(o1.view(B * L, -1)).view(torch.int16))
