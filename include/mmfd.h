@@ -117,6 +117,12 @@ int mmfd_gemm_splits(const mmfd_gemm_args* args);
    test_kernels_gpu.py); mode 0 = the fp32 MFMA (v_mfma_f32_16x16x4f32). Used only when
    workspace_bytes covers mmfd_gemm_workspace_bytes. Returns the previous mode. */
 int mmfd_set_fp32_gemm_mode(int mode);
+/* whether mmfd_gemm runs these arguments as a split-operand fp32 GEMM (given the workspace it asks
+   for): 0 = no (fp32 MFMA or bf16 path), 2 = the fused-plane kernel (all three planes of both
+   operands staged per 32-deep K-step, the default), 1 = the segmented kernel (the K loop once per
+   plane pair; env MMFD_X6_SEGMENTED). The host-side planning of which tensors may exist only as
+   planes (mmfd.kernels.x6_ok) asks this, so it honours every switch the library does. */
+int mmfd_gemm_runs_split(const mmfd_gemm_args* args);
 /* fp32 [rows][ld] -> bf16 planes [3][rows][cols] (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid);
    cols % 8 == 0, 16-B aligned rows) */
 int mmfd_split3(int64_t rows, int64_t cols, const float* x, int64_t ld, void* planes, mmfd_stream_t stream);

@@ -31,6 +31,10 @@ struct X6Args { int nkt; uint32_t pa, pb; };
 constexpr uint32_t X6_CA = 0x121;  // A planes per segment (2 bits each): m h l h m h
 constexpr uint32_t X6_CB = 0x049;  // B planes per segment:                m l h m h h
 constexpr uint32_t X6_RS = 0x25;   // segments whose A plane appears once (m, l, h): row sums of op(A)
+// split-operand fp32 GEMM with fused planes (gemm_x6f.hip): launches gemm256_x6f_kernel for the
+// operand layout of `a` (A / B = the bf16 planes pa / pb, x6.nkt = 32-deep K-steps in all)
+void dispatch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
+                  int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
 }  // namespace mmfd_gemmx
 
 namespace {
@@ -39,6 +43,7 @@ using mmfd_gemmx::X6Args;
 using mmfd_gemmx::X6_CA;
 using mmfd_gemmx::X6_CB;
 using mmfd_gemmx::X6_RS;
+using mmfd_gemmx::dispatch_x6f;
 
 
 // Tile geometry: 256 (M) x 128 (N) x 128 B of K (64 bf16 / 32 fp32), 8 waves as 4 (M) x 2 (N), each
@@ -331,5 +336,403 @@ __device__ __forceinline__ uint4 load_frag(const char* img, int sub, int kc, int
   }
 }
 
+
+// =================================================================================================
+// 256x256 kernel ("G8", bf16 and fp32 operands): 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns four
+// 64x32 quadrants (mq, nq): rows mq*128 + wr*64 + [0,64), cols nq*128 + wc*32 + [0,32). Each K-tile
+// (128 B of K per row: 64 bf16 / 32 fp32) is
+// staged as four 16-KB half-tiles (A rows [0,128) / [128,256), B cols [0,128) / [128,256)) into
+// one of two LDS buffers by LDS-DMA, and consumed in four phases, one quadrant (16 MFMAs) each:
+//   phase 0: (0,0) reads A-h0, B-h0   phase 1: (0,1) reads B-h1
+//   phase 2: (1,1) reads A-h1         phase 3: (1,0) reads B-h0
+// Every phase refills the half-tile whose last read was the previous phase (one half-tile = two
+// DMA pieces per wave), so three half-tiles stay in flight across the barriers; the only wait is
+// a counted vmcnt(6) in phase 3. The two wave rows run one barrier apart (ping-pong): while one
+// row issues its LDS reads and DMA the other row's MFMAs run.
+// =================================================================================================
+constexpr int G8_HALF = 16384;
+constexpr int G8_LDS = 128 * (256 + 4) * 4;  // >= 2 buffers x 4 half-tiles (128 KB); 128-row epilogue staging
+constexpr int G8_BM = 256, G8_BN = 256;
+template <typename T> struct G8T { static constexpr int BK = ROWB / (int)sizeof(T); };  // K per K-tile
+
+__device__ __forceinline__ void g8_pre_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS reads retired (WAR vs the next refill)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void g8_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename T, int LAYOUT>
+__device__ __forceinline__ void g8_frag_a(uint4 (&a)[4][2], const char* img, int wr, int lane) {
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<T, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
+}
+// B fragment j (j = 0, 1) of the wave's 32 columns gathers the 4-column units 2p + j (p = 0..3),
+// and the MFMA runs with swapped operands (acc = B-fragment x A-fragment = the C^T block): lane
+// (g, ci) of accumulator (i, j) then holds row i*16 + ci, columns 8g + 4j .. +3, i.e. every lane
+// owns 8 CONSECUTIVE columns of a row (fragment 0 the low four) — one 16-byte bf16 chunk for the
+// register epilogue. The K-contiguous B image uses the SW = 1 swizzle under which these
+// ds_read_b128 are conflict-free; the MN-contiguous (transposed ds_read_b64_tr_b16) B reads are
+// 2-way (each 16-B chunk is read in one half only), well inside the LDS budget of a K-tile.
+// fp32 operands: the same column interleave, the 16x16x4 fragment being 4 consecutive k of the
+// row (layout 0: one ds_read_b128; layout 1: 4 ds_read_b32 down the K rows of the column)
+template <typename T, int LAYOUT>
+__device__ __forceinline__ uint4 g8_load_b(const char* img, int wc, int j, int kc, int lane) {
+  using I = Img<T, LAYOUT, 128, 1>;
+  const int g = lane >> 4, i = lane & 15;
+  if (LAYOUT == 0) {
+    const int row = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
+    return lds_read16(img, row * ROWB + (I::swz(row, kc * 4 + g) << 4));
+  } else if (sizeof(T) == 2) {
+    const int q = i >> 2, p = i & 3;
+    const int r1 = kc * 32 + 8 * g + q, r2 = r1 + 4;
+    const int u = wc * 8 + 2 * p + j;  // 8-B unit (4 bf16)
+    const uint2 a = lds_read_tr16(img + r1 * I::RBY + (I::swz(r1, u >> 1) << 4) + ((u & 1) << 3));
+    const uint2 b = lds_read_tr16(img + r2 * I::RBY + (I::swz(r2, u >> 1) << 4) + ((u & 1) << 3));
+    return make_uint4(a.x, a.y, b.x, b.y);
+  } else {
+    const int col = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
+    uint32_t v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = kc * 16 + 4 * g + s;
+      v[s] = *reinterpret_cast<const uint32_t*>(img + row * I::RBY + (I::swz(row, col >> 2) << 4) + (col & 3) * 4);
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+template <typename T, int LAYOUT>
+__device__ __forceinline__ void g8_frag_b(uint4 (&b)[2][2], const char* img, int wc, int lane) {
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j][kc] = g8_load_b<T, LAYOUT>(img, wc, j, kc, lane);
+}
+template <typename T>
+__device__ __forceinline__ void g8_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][2], const uint4 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) Mma<T>::run(acc[i][j], b[j][kc], a[i][kc]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// two quadrants sharing the A fragments (one phase of the two-phase schedule)
+template <typename T>
+__device__ __forceinline__ void g8_mma2(f32x4 (&acc0)[4][2], f32x4 (&acc1)[4][2], const uint4 (&a)[4][2],
+                                        const uint4 (&b0)[2][2], const uint4 (&b1)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        Mma<T>::run(acc0[i][j], b0[j][kc], a[i][kc]);
+        Mma<T>::run(acc1[i][j], b1[j][kc], a[i][kc]);
+      }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <typename T>
+__device__ __forceinline__ float g8_sum16b(uint4 x) {  // the elements of one 16-B chunk
+  if (sizeof(T) == 4)
+    return (__uint_as_float(x.x) + __uint_as_float(x.y)) + (__uint_as_float(x.z) + __uint_as_float(x.w));
+  return ((__uint_as_float(x.x << 16) + __uint_as_float(x.x & 0xffff0000u)) +
+          (__uint_as_float(x.y << 16) + __uint_as_float(x.y & 0xffff0000u))) +
+         ((__uint_as_float(x.z << 16) + __uint_as_float(x.z & 0xffff0000u)) +
+          (__uint_as_float(x.w << 16) + __uint_as_float(x.w & 0xffff0000u)));
+}
+// wave wc sums A subtile wc of the half-tile (its own two LDS reads: a runtime subtile index into
+// the fragment registers would push them to scratch)
+template <typename T, int LAYOUT>
+__device__ __forceinline__ float g8_rowsum(const char* img, int wr, int wc, int lane) {
+  return g8_sum16b<T>(load_frag<T, LAYOUT, 128>(img, wr * 4 + wc, 0, lane)) +
+         g8_sum16b<T>(load_frag<T, LAYOUT, 128>(img, wr * 4 + wc, 1, lane));
+}
+
+// Diagnostic build only (-DMMFD_G8_STAMPS, tools/g8_stamps.py): per-wave s_memtime stamps at
+// the phase boundaries of the 256x256 kernel, to a buffer no computation reads.
+#ifdef MMFD_G8_STAMPS
+constexpr int G8_NSTAMP = 8;
+__device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
+#define G8_STAMP(k)                                                                                    \
+  do {                                                                                                 \
+    const uint64_t t__ = __builtin_amdgcn_s_memtime();                                                \
+    const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                                 \
+    if (lane == 0 && b__ < 16384) g8_stamps[(b__ * 8 + wave) * G8_NSTAMP + (k)] = t__;                \
+  } while (0)
+#else
+#define G8_STAMP(k) do { } while (0)
+#endif
+
+// Epilogue of the 256x256 kernels (gemm256_kernel, gemm256_x6f_kernel): two passes of 128 rows
+// (quadrant row mq = pass); every wave stages its fp32 accumulators, then all threads apply the
+// epilogue to 8-column chunks with 16-B accesses
+template <typename TC, bool PRE>
+__device__ __forceinline__ void g8_epilogue(f32x4 (&acc)[2][2][4][2], char* smem, const EpiArgs& e, TC* __restrict__ C,
+                                            int64_t ldc, float* __restrict__ ws, int split, int64_t M, int64_t N,
+                                            float alpha, int64_t m0, int64_t n0, int tid, int lane, int wave,
+                                            int wr, int wc) {
+  constexpr int LDC = G8_BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
+  const int g = lane >> 4, ci = lane & 15;
+  const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
+  float* slab = ws ? ws + (int64_t)split * M * N : nullptr;
+  // fast path (full tile, 16-B aligned operands, no split-K slab): every thread owns the same 8
+  // columns in all its rows, so the bias is loaded once; per pass all residual / aux / C loads of
+  // the thread's 8 rows are issued before any math or store (one wait per pass, not per row)
+  if (!slab && e.vec && m0 + G8_BM <= M && n0 + G8_BN <= N) {
+    const int c8 = (tid % (G8_BN / 8)) * 8;
+    const int64_t col = n0 + c8;
+    float bia[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) bia[u] = e.bias ? e.bias[col + u] : 0.f;
+    const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
+    const bool fwd_act = e.act == MMFD_ACT_GELU || e.act == MMFD_ACT_RELU;
+    // one pass per 128-row half; a lambda per pass (not an unrolled loop, whose body is too big to
+    // unroll) keeps every accumulator index a compile-time constant
+    auto pass = [&](auto mqc) {
+      constexpr int mq = decltype(mqc)::value;
+      if constexpr (PRE) {
+        // exactly one operand stream (residual OR aux OR C; chosen on the host): all IT rows of it
+        // are loaded before the accumulators are staged, so their HBM latency overlaps the
+        // staging and its barrier instead of being paid once per row group
+        constexpr int IT = 128 * (G8_BN / 8) / NT;
+        const int lr0 = tid / (G8_BN / 8);
+        const int64_t rstep = NT / (G8_BN / 8);
+        const int64_t rbase = m0 + mq * 128;
+        const int oc = lr0 * (int)ldc + c8, orr = lr0 * (int)e.ldr + c8, oa = lr0 * (int)e.ldaux + c8;
+        TC* cp = C + rbase * ldc + n0 + oc;
+        const int64_t cs = rstep * ldc, rs = rstep * e.ldr, xs = rstep * e.ldaux;
+        const bool res = e.residual != nullptr;
+        const TC* lp = res ? reinterpret_cast<const TC*>(e.residual) + rbase * e.ldr + n0 + orr
+                           : bwd_act ? reinterpret_cast<const TC*>(e.aux) + rbase * e.ldaux + n0 + oa : cp;
+        const int64_t ls = res ? rs : (bwd_act ? xs : cs);
+        Raw8<TC> pre[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) pre[k].load(lp + k * ls);
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+                  acc[mq][nq][i][j];
+        __syncthreads();
+        TC* ap = (fwd_act && e.aux) ? reinterpret_cast<TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+        const uint64_t hidx = (uint64_t)(rbase + lr0) * (uint64_t)N + (uint64_t)col;
+        const float* src = ct + lr0 * LDC + c8;
+#pragma unroll
+        for (int kk = 0; kk < IT; ++kk) {
+          const float4 a4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC);
+          const float4 b4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC + 4);
+          float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
+          float t[8];
+          pre[kk].get(t);
+          if (res && e.res_first) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (fwd_act) {
+            if (ap) V8<TC>::store(ap + kk * xs, z);
+            if (e.act == MMFD_ACT_GELU) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+            }
+          } else if (bwd_act) {
+            if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+            }
+          } else if (e.act >= MMFD_ACT_TANH) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = act_tail_f(e.act, z[u]);
+          }
+          if (e.p > 0.f) {
+            const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
+          }
+          if (res && !e.res_first) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (!res && !bwd_act) {  // the stream is C: beta * C
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+          }
+          V8<TC>::store(cp + kk * cs, z);
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+                acc[mq][nq][i][j];
+      if (mq == 0) G8_STAMP(3);
+      __syncthreads();
+      if (mq == 0) G8_STAMP(4);
+      constexpr int IT = 128 * (G8_BN / 8) / NT;  // 8 rows per thread, in two groups of 4
+      // every thread owns 8 columns of rows lr0 + 16 k (k < IT): the operand / output row pointers
+      // advance by a scalar stride (no per-row 64-bit address math), every epilogue branch is
+      // uniform, and the residual / aux / C loads of GI rows are in flight before their math
+      const int lr0 = tid / (G8_BN / 8);
+      const int64_t rstep = NT / (G8_BN / 8);  // 16 rows between a thread's rows
+      const int64_t rbase = m0 + mq * 128;     // uniform part of the row
+      // uniform (scalar) tile bases + 32-bit per-lane offsets (host-checked: operands < 2^31 elements)
+      const int oc = lr0 * (int)ldc + c8, orr = lr0 * (int)e.ldr + c8, oa = lr0 * (int)e.ldaux + c8;
+      TC* cp = C + rbase * ldc + n0 + oc;
+      const TC* rp = e.residual ? reinterpret_cast<const TC*>(e.residual) + rbase * e.ldr + n0 + orr : nullptr;
+      const TC* xp = bwd_act ? reinterpret_cast<const TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+      TC* ap = (fwd_act && e.aux) ? reinterpret_cast<TC*>(e.aux) + rbase * e.ldaux + n0 + oa : nullptr;
+      const uint64_t hidx = (uint64_t)(rbase + lr0) * (uint64_t)N + (uint64_t)col;
+      const int64_t cs = rstep * ldc, rs = rstep * e.ldr, xs = rstep * e.ldaux;
+      const float* src = ct + lr0 * LDC + c8;
+      constexpr int GI = 2;
+#pragma unroll
+      for (int k0 = 0; k0 < IT; k0 += GI) {
+        Raw8<TC> rres[GI], raux[GI], rc[GI];
+#pragma unroll
+        for (int k = 0; k < GI; ++k) {
+          const int kk = k0 + k;
+          if (rp) rres[k].load(rp + kk * rs);
+          if (xp) raux[k].load(xp + kk * xs);
+          if (e.beta != 0.f) rc[k].load(cp + kk * cs);
+        }
+#pragma unroll
+        for (int k = 0; k < GI; ++k) {
+          const int kk = k0 + k;
+          const float4 a4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC);
+          const float4 b4 = *reinterpret_cast<const float4*>(src + kk * rstep * LDC + 4);
+          float z[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] = fmaf(alpha, z[u], bia[u]);
+          float t[8];
+          if (rp && e.res_first) {
+            rres[k].get(t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (fwd_act) {
+            if (ap) V8<TC>::store(ap + kk * xs, z);
+            if (e.act == MMFD_ACT_GELU) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = gelu_f(z[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = fmaxf(z[u], 0.f);
+            }
+          } else if (xp) {
+            raux[k].get(t);
+            if (e.act == MMFD_ACT_GELU_BWD) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] *= gelu_grad_f(t[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) z[u] = t[u] > 0.f ? z[u] : 0.f;
+            }
+          } else if (e.act >= MMFD_ACT_TANH) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = act_tail_f(e.act, z[u]);
+          }
+          if (e.p > 0.f) {
+            const uint64_t base = hidx + (uint64_t)(kk * rstep) * (uint64_t)N;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = (mmfd_hash_k(seed, base + u) < e.thr) ? 0.f : z[u] * e.keep_scale;
+          }
+          if (rp && !e.res_first) {
+            rres[k].get(t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] += t[u];
+          }
+          if (e.beta != 0.f) {
+            rc[k].get(t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) z[u] = fmaf(e.beta, t[u], z[u]);
+          }
+          if (std::is_same<TC, float>::value && e.pl) {
+            planes_store8(e, N, rbase + lr0 + kk * rstep, col, z);
+            if (!e.c_out) continue;
+          }
+          V8<TC>::store(cp + kk * cs, z);
+        }
+      }
+      __syncthreads();
+      if (mq == 0) G8_STAMP(5);
+      }
+    };
+    pass(std::integral_constant<int, 0>{});
+    pass(std::integral_constant<int, 1>{});
+    G8_STAMP(6);
+#ifdef MMFD_G8_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    G8_STAMP(7);
+#endif
+    return;
+  }
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq) {
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<f32x4*>(ct + (wr * 64 + i * 16 + ci) * LDC + nq * 128 + wc * 32 + 8 * g + 4 * j) =
+              acc[mq][nq][i][j];
+    __syncthreads();
+    const int64_t rbase = m0 + mq * 128;
+    for (int idx = tid; idx < 128 * (G8_BN / 8); idx += NT) {
+      const int lr = idx / (G8_BN / 8), c8 = (idx % (G8_BN / 8)) * 8;
+      const int64_t row = rbase + lr, col = n0 + c8;
+      if (row >= M || col >= N) continue;
+      const float* src = ct + lr * LDC + c8;
+      const float4 a4 = *reinterpret_cast<const float4*>(src), b4 = *reinterpret_cast<const float4*>(src + 4);
+      float vv[8] = {alpha * a4.x, alpha * a4.y, alpha * a4.z, alpha * a4.w,
+                     alpha * b4.x, alpha * b4.y, alpha * b4.z, alpha * b4.w};
+      const bool full = col + 8 <= N;
+      if (slab) {
+        if (full && (N % 4) == 0) {
+          *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          *reinterpret_cast<float4*>(slab + row * N + col + 4) = make_float4(vv[4], vv[5], vv[6], vv[7]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (col + u < N) slab[row * N + col + u] = vv[u];
+        }
+      } else if (full && e.vec) {
+        epilogue_store8<TC>(e, C, ldc, N, row, col, vv, seed);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (col + u < N) epilogue_store<TC>(e, C, ldc, N, row, col + u, vv[u], seed);
+      }
+    }
+    __syncthreads();
+  }
+}
 
 }  // namespace

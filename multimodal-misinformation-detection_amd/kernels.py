@@ -115,6 +115,7 @@ SIGNATURES = {
     "mmfd_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmArgs)]),
     "mmfd_set_fp32_gemm_mode": (_I, [_I]),
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
+    "mmfd_gemm_runs_split": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
     "mmfd_layernorm_fwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP, _VP]),
     "mmfd_layernorm_bwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP,
@@ -312,14 +313,9 @@ class GemmProbe:
 
 
 def _x6(a):
-    """whether mmfd_gemm runs this fp32 product on split bf16 operands (gemm.hip x6_plan)"""
-    if fp32_gemm_mode() != 1 or a.dtype != F32 or a.c_dtype != F32:
-        return False
-    ra, ca = (a.K, a.M) if a.trans_a else (a.M, a.K)
-    rb, cb = (a.K, a.N) if a.trans_b else (a.N, a.K)
-    if ca % 8 or cb % 8 or ((a.trans_a or a.trans_b) and a.K % 64):
-        return False
-    return 6 * max(ra * ca, rb * cb) < (1 << 31) - 4096
+    """whether mmfd_gemm runs this fp32 product on split bf16 operands: 0 no, 2 fused-plane kernel,
+    1 segmented kernel (the library's own decision, mmfd_gemm_runs_split)"""
+    return lib().mmfd_gemm_runs_split(ctypes.byref(a))
 
 
 _FP32_MODE = None
@@ -354,8 +350,11 @@ def _kernel_name(a, split):
         streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD)) + int(a.beta != 0.0)
         pre = a.c_dtype == BF16 and streams == 1 and not split
         x6 = _x6(a)
-        base = (f"gemm256_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
-                f"{'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
+        if x6 == 2:
+            base = f"gemm256_x6f_kernel<{a.trans_a}, {a.trans_b}>"
+        else:
+            base = (f"gemm256_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
+                    f"{'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
     else:
         base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")
@@ -449,17 +448,20 @@ def split3(x, out=None):
 
 
 def x6_ok(M, N, K, trans_a=False, trans_b=False):
-    """whether mmfd_gemm runs this fp32 product on split operands (gemm.hip x6_plan + use_g8 +
-    mfma_ok for contiguous operands)"""
-    if fp32_gemm_mode() != 1 or min(M, N, K) < 16:
+    """whether mmfd_gemm runs this fp32 product (contiguous operands) on split operands — asked of
+    the library itself (mmfd_gemm_runs_split: x6_plan + use_g8 + mfma_ok, every env switch
+    included), so a producer never skips an fp32 output that a consumer would then read"""
+    if fp32_gemm_mode() != 1 or min(M, N, K) < 1:
         return False
-    if M >= 4096 and (N <= 128 or K < 64):
-        return False
-    ra, ca = (K, M) if trans_a else (M, K)
-    rb, cb = (K, N) if trans_b else (N, K)
-    if ca % 8 or cb % 8 or ((trans_a or trans_b) and K % 64):
-        return False
-    return 6 * max(ra * ca, rb * cb) < (1 << 31) - 4096
+    a = GemmArgs()
+    a.dtype = a.c_dtype = F32
+    a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.A = a.B = a.C = 1 << 20  # placeholder 16-B aligned pointers: only the shapes are inspected
+    a.lda = M if trans_a else K
+    a.ldb = N if trans_b else K
+    a.ldc = N
+    return lib().mmfd_gemm_runs_split(ctypes.byref(a)) != 0
 
 
 def split_eligible(x):

@@ -448,7 +448,8 @@ def test_adamw_matches_torch():
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-@pytest.mark.parametrize("shape", [(512, 768, 768), (1000, 520, 200), (768, 256, 4096), (256, 2304, 65536)])
+@pytest.mark.parametrize("shape", [(512, 768, 768), (1000, 520, 200), (300, 264, 1056), (768, 256, 4096),
+                                   (256, 2304, 65536)])
 def test_gemm_fp32_split_operands_error_matches_fp32_mfma(layout, shape):
     """fp32 GEMMs on split bf16 operands (x = hi + mid + lo, six products accumulated small-first,
     include/mmfd.h mmfd_set_fp32_gemm_mode) against an fp64 product: the error may not exceed the
@@ -457,8 +458,8 @@ def test_gemm_fp32_split_operands_error_matches_fp32_mfma(layout, shape):
     segments (the tall K = 65536 weight-gradient shape) and every operand layout."""
     M, N, Kd = shape
     ta, tb = layout[0] == "t", layout[1] == "t"
-    if (ta or tb) and Kd % 64:
-        pytest.skip("MN-contiguous operands need whole 64-row K tiles on the split path (fp32 MFMA used)")
+    if not K.x6_ok(M, N, Kd, ta, tb):
+        pytest.skip("MN-contiguous operands need whole 32-row K-steps on the split path (fp32 MFMA used)")
     g = torch.Generator().manual_seed(M + N + Kd)
     A = torch.randn((Kd, M) if ta else (M, Kd), generator=g).to(DEV)
     B = (torch.randn((Kd, N) if tb else (N, Kd), generator=g) * 0.05).to(DEV)
