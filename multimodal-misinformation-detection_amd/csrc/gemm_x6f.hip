@@ -37,6 +37,22 @@ namespace {
 // vmcnt(6) at the end of each read phase). The two wave rows run one barrier apart (ping-pong) as
 // in gemm256_kernel: per phase one row issues its reads / DMA while the other runs 48 MFMAs.
 // =================================================================================================
+// Diagnostic build only (-DMMFD_XF_STAMPS, tools/xf_stamps.py): s_memtime at the phase boundaries of
+// one mid-loop K-step, per wave, into a buffer no computation reads.
+#ifdef MMFD_XF_STAMPS
+__device__ uint64_t xf_stamps[4096 * 8 * 16];
+#define XF_STAMP(k)                                                                                   \
+  do {                                                                                                \
+    if (t == xf_t) {                                                                                  \
+      const uint64_t t__ = __builtin_amdgcn_s_memtime();                                             \
+      const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                              \
+      if (lane == 0 && b__ < 4096) xf_stamps[(b__ * 8 + wave) * 16 + (k)] = t__;                     \
+    }                                                                                                 \
+  } while (0)
+#else
+#define XF_STAMP(k) do { } while (0)
+#endif
+
 constexpr int XF_SLOT = 8192;
 constexpr int XF_BK = 32;  // K per step
 
@@ -104,10 +120,12 @@ __device__ __forceinline__ uint4 xf_frag_b(const char* img, int wc, int j, int l
 // them past the phase's barrier
 __device__ __forceinline__ void xf_add(f32x4& acc, const f32x4& t) {
   acc[0] += t[0]; acc[1] += t[1]; acc[2] += t[2]; acc[3] += t[3];
-  asm volatile("" : "+v"(acc));
 }
+#ifndef XF_PRIO_STATIC
+#define XF_PRIO_STATIC 1
+#endif
 __device__ __forceinline__ void xf_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][3], const uint4 (&b)[2][3]) {
-  __builtin_amdgcn_s_setprio(1);
+  if (!XF_PRIO_STATIC) __builtin_amdgcn_s_setprio(1);
   f32x4 p0, p1;  // the previous subtile's sums
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -130,11 +148,26 @@ __device__ __forceinline__ void xf_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][3
     Mma<bf16>::run(t1, b[1][0], a[i][0]);
     p0 = t0;
     p1 = t1;
+    if (i > 0) {
+      // the previous subtile's 8 adds one per MFMA gap after this subtile's first four products
+      // (by then the chains they read have retired: no wait states; at most one 4-cycle VALU op
+      // beside each 16-cycle MFMA)
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   xf_add(acc[3][0], p0);
   xf_add(acc[3][1], p1);
-  __builtin_amdgcn_s_setprio(0);
+  // keep every add inside the phase (an input-only use: the compiler may not sink them past the
+  // barrier into the next iteration, where the sums would stay live and spill fragments)
+  asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]), "v"(acc[2][0]), "v"(acc[2][1]),
+               "v"(acc[3][0]), "v"(acc[3][1]));
+  if (!XF_PRIO_STATIC) __builtin_amdgcn_s_setprio(0);
 }
 
 // sum of the 3 x 8 bf16 values of one A fragment's planes (hi + mid + lo = the fp32 elements)
@@ -162,6 +195,9 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
   const int nst = x6.nkt;  // K-steps in all (host: ceil(K / 32))
   const int st0 = split * steps_per_split;
   const int nk = min(nst, st0 + steps_per_split) - st0;
+#ifdef MMFD_XF_STAMPS
+  const int xf_t = min(4, nk - 1);
+#endif
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -210,6 +246,9 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
   }
   g8_barrier();
   if (wr == 1) g8_barrier();  // stagger the second wave row by one barrier
+  // static priority for the second-dispatched half (waves 4-7), set once: without it that half
+  // loses every issue arbitration to its SIMD partner (MI355X_MICROARCH.md, two waves per SIMD, 4)
+  if (XF_PRIO_STATIC && wr == 1) __builtin_amdgcn_s_setprio(1);
 
   // fused row sums of op(A) (bias gradient): as gemm256_kernel, per K-step; wave wc sums A
   // subtile wc of each A half-tile (all three planes: hi + mid + lo = the fp32 value)
@@ -246,6 +285,7 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
     {
       int ln = lane;
       asm volatile("" : "+v"(ln));  // recompute the fragment addresses here (no hoisted copies)
+      XF_STAMP(0);
       const char* ia = slot(0, t);
       const char* ib = slot(2, t);
 #pragma unroll
@@ -258,14 +298,18 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
       if (rs_t) XF_ROWSUM(rs0);
       if (t + 1 < nk) issue(2, t + 1);
       wait_next(t, false);
+      XF_STAMP(1);
       g8_pre_barrier();
+      XF_STAMP(2);
       xf_mma(acc[0][0], fa, fb);
+      XF_STAMP(3);
       g8_barrier();
     }
     // phase 1: quadrant (0,1) from B-h1 (A-h0 kept)
     {
       int ln = lane;
       asm volatile("" : "+v"(ln));  // recompute the fragment addresses here (no hoisted copies)
+      XF_STAMP(4);
       const char* ib = slot(3, t);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
@@ -273,14 +317,18 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
         for (int j = 0; j < 2; ++j) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
       if (t + 1 < nk) issue(0, t + 1);
       wait_next(t, false);
+      XF_STAMP(5);
       g8_pre_barrier();
+      XF_STAMP(6);
       xf_mma(acc[0][1], fa, fb);
+      XF_STAMP(7);
       g8_barrier();
     }
     // phase 2: quadrant (1,1) from A-h1 (B-h1 kept)
     {
       int ln = lane;
       asm volatile("" : "+v"(ln));  // recompute the fragment addresses here (no hoisted copies)
+      XF_STAMP(8);
       const char* ia = slot(1, t);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
@@ -289,14 +337,18 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
       if (rs_t) XF_ROWSUM(rs1);
       if (t + 1 < nk) issue(3, t + 1);
       wait_next(t, true);
+      XF_STAMP(9);
       g8_pre_barrier();
+      XF_STAMP(10);
       xf_mma(acc[1][1], fa, fb);
+      XF_STAMP(11);
       g8_barrier();
     }
     // phase 3: quadrant (1,0) from B-h0(t) (A-h1 kept)
     {
       int ln = lane;
       asm volatile("" : "+v"(ln));  // recompute the fragment addresses here (no hoisted copies)
+      XF_STAMP(12);
       const char* ib = slot(2, t);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
@@ -304,12 +356,16 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
         for (int j = 0; j < 2; ++j) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
       if (t + 1 < nk) issue(1, t + 1);
       wait_next(t, false);
+      XF_STAMP(13);
       g8_pre_barrier();
+      XF_STAMP(14);
       xf_mma(acc[1][0], fa, fb);
+      XF_STAMP(15);
       g8_barrier();
     }
   }
 
+  if (XF_PRIO_STATIC && wr == 1) __builtin_amdgcn_s_setprio(0);
   if (wr == 0) g8_barrier();  // re-align the wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -330,7 +386,15 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #undef XF_ROWSUM
 }
 
+
+
 }  // namespace
+
+#ifdef MMFD_XF_STAMPS
+extern "C" int mmfd_debug_xf_stamps(void* host_dst, int64_t bytes) {
+  return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(xf_stamps), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 namespace mmfd_gemmx {
 template <int TA, int TB>

@@ -35,11 +35,15 @@ class GradAllReduce:
     kernels; they are parameters only so the bucketing + collective logic can be exercised on the
     CPU (gloo) in tests."""
 
-    def __init__(self, bucket_mb: float = 32.0, group=None, pack=_pack, unpack=_unpack):
+    def __init__(self, bucket_mb: float = 32.0, group=None, pack=_pack, unpack=_unpack, force=False):
+        """`force`: run the bucketing, packing and collectives even with one rank (tests and the DP
+        overhead measurement on a one-GPU box; a world-size-1 all-reduce leaves the values as they are)"""
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
         self.group = group
+        self.force = bool(force)
         self._bufs = {}
         self._pack, self._unpack = pack, unpack
+        self.last_buckets = {}
         self.begin()
 
     # ---- per-step protocol ------------------------------------------------------------------------
@@ -88,6 +92,7 @@ class GradAllReduce:
                 n = g.numel()
                 self._unpack(buf[off:off + n], p.grad if p.grad is not None else g, 1.0 / world)
                 off += n
+        self.last_buckets = dict(self._nbucket)  # buckets per stream of the step just finished
         self.begin()
 
     def broadcast_params(self, params, src=0):
@@ -126,7 +131,7 @@ class GradAllReduce:
 
     # ---- internals -----------------------------------------------------------------------------------
     def _active(self):
-        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+        return dist.is_initialized() and (self.force or dist.get_world_size(self.group) > 1)
 
     def _flush(self, key):
         items, n = self._pending.pop(key, [[], 0])

@@ -183,7 +183,15 @@ class FusionTrainer:
         if self.dp is not None:
             self.dp.finish()
         self.optimizer.step()
-        return (loss, outs) if return_outputs else loss
+        # detached results: a returned loss / logits still holding their grad_fn would keep this
+        # step's autograd graph — and the AccumulateGrad nodes of every parameter, bound to the
+        # streams of this step — alive into the next step, where the text encoder's backward runs
+        # on the other stream (torch's "AccumulateGrad node's stream does not match" warning and
+        # an extra cross-stream synchronisation)
+        loss = loss.detach()
+        if return_outputs:
+            return loss, _detach_outs(outs)
+        return loss
 
     # ---- the whole step as one HIP graph ------------------------------------------------------------
     def capture(self, batch, warmup=2):
@@ -242,13 +250,25 @@ class FusionTrainer:
                 m.train(w)
 
 
+def _detach_outs(o):
+    if torch.is_tensor(o):
+        return o.detach()
+    if isinstance(o, (tuple, list)):
+        return type(o)(_detach_outs(x) for x in o)
+    return o
+
+
 def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders=False, lr=1e-4, dp=None,
-                   seed=42, rank=0):
+                   seed=42, rank=0, encoder_dropout=None):
     """bert-base-uncased + ViT-B/16 + the fusion head at 768/768 (BASELINE configs 2-4), random init
     from `seed` (the same on every rank; with `dp` rank 0's weights are broadcast anyway); the
-    dropout streams are offset per rank so replicas draw independent masks."""
+    dropout streams are offset per rank so replicas draw independent masks. `dropout` is the head's
+    (model.py dropout=0.1); the encoders keep their HF configs' own (BERT 0.1, ViT 0.0) unless
+    `encoder_dropout` overrides both."""
     torch.manual_seed(seed)
-    text = BertModel(BertConfig()).to(device)
+    bc = BertConfig() if encoder_dropout is None else BertConfig(hidden_dropout_prob=encoder_dropout,
+                                                                  attention_probs_dropout_prob=encoder_dropout)
+    text = BertModel(bc).to(device)
     image = ViTModel(ViTConfig()).to(device)
     head = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768, embed_dim=256, num_heads=8,
                                         dropout=dropout, hidden_dim=64, num_classes=3).to(device)

@@ -96,3 +96,120 @@ def test_dp_two_ranks_match_full_batch():
         for r in range(world):
             e = abs(res[r][k] - g).max() / scale
             assert e < 2e-4, f"rank {r} {k}: {e:.2e}"
+
+
+# ---- full size: bert-base + ViT-B/16 + head, default 32 MB buckets, two encoder streams ----------
+def _worker_full(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.dp import GradAllReduce
+        from mmfd.train import build_flagship
+        from tests.smoke_impl import FULL, tiny_batch
+        dp = GradAllReduce()  # the default 32 MB buckets, as bench.py / train.py use them
+        assert dp.bucket_elems == 32 * (1 << 20) // 4
+        # each rank from its OWN seed (rank 0's weights are broadcast), dropout off for the comparison
+        tr = build_flagship("cuda", "fp32", dropout=0.0, dp=dp, seed=42 + 11 * rank, rank=rank, encoder_dropout=0.0)
+        assert tr.concurrent  # text / image encoders on two HIP streams: buckets per stream
+        b = _half(tiny_batch(2, cfg=FULL, seed=31), rank, world)
+        tr.step({k: v.cuda() for k, v in b.items()})
+        torch.cuda.synchronize()
+        q.put((rank, _grads(tr), dict(dp.last_buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_full_size_default_buckets_two_streams():
+    """config 4 at full size on the box's one GPU: 2 gloo ranks, bert-base + ViT-B/16 + the head at
+    B = 1 pair per rank, the default 32 MB per-stream buckets over the 796 MB of fp32 gradients and
+    both encoder streams; the averaged gradients equal the single-process B = 2 step's within 2e-4
+    of each tensor's max (fp32, dropout off)."""
+    from mmfd.train import build_flagship
+    from tests.smoke_impl import FULL, tiny_batch
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_full, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, nb = {}, {}
+    for _ in range(world):
+        r, g1, buckets = q.get(timeout=600)
+        res[r], nb[r] = g1, buckets
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    print(f"buckets per stream: {nb[0]}", flush=True)
+    assert len(nb[0]) == 2 and sum(nb[0].values()) >= 20, nb[0]  # buckets on both streams
+    tr = build_flagship("cuda", "fp32", dropout=0.0, seed=42, encoder_dropout=0.0)
+    tr.step({k: v.cuda() for k, v in tiny_batch(2, cfg=FULL, seed=31).items()})
+    torch.cuda.synchronize()
+    full = _grads(tr)
+    floor = 1e-3 * max(abs(g).max() for g in full.values() if g is not None)
+    worst = 0.0
+    for k, g in full.items():
+        if g is None:
+            continue
+        scale = max(abs(g).max(), floor)
+        for r in range(world):
+            e = abs(res[r][k] - g).max() / scale
+            worst = max(worst, e)
+            assert e < 2e-4, f"rank {r} {k}: {e:.2e}"
+    print(f"full-size DP (2 ranks x 1 pair vs 1 x 2 pairs): worst gradient error {worst:.2e}, buckets {nb[0]}")
+
+
+# ---- RCCL: ProcessGroupNCCL with one rank, the overlapped all-reduce forced on ----------------------
+def _worker_nccl(port, q):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from mmfd.dp import GradAllReduce
+        from mmfd.train import FusionTrainer, build_flagship
+        from tests.smoke_impl import FULL, build_pair, tiny_batch
+        out = {}
+        # tiny models with 50 KB buckets: many buckets in flight on both encoder streams
+        t_dp, _ = build_pair("fp32", dropout=0.0, seed=5)
+        t_ref, _ = build_pair("fp32", dropout=0.0, seed=5)
+        dp = GradAllReduce(bucket_mb=0.05, force=True)
+        tr_dp = FusionTrainer(t_dp.text_encoder, t_dp.image_encoder, t_dp.head, lr=1e-3, precision="fp32", dp=dp)
+        tr_ref = FusionTrainer(t_ref.text_encoder, t_ref.image_encoder, t_ref.head, lr=1e-3, precision="fp32")
+        # full size with the default 32 MB buckets
+        f_dp = build_flagship("cuda", "fp32", dropout=0.0, seed=42, dp=GradAllReduce(force=True))
+        f_ref = build_flagship("cuda", "fp32", dropout=0.0, seed=42)
+        for name, a, b, batches in (("tiny", tr_dp, tr_ref, [tiny_batch(4, seed=21), tiny_batch(4, seed=22)]),
+                                    ("full", f_dp, f_ref, [tiny_batch(1, cfg=FULL, seed=41),
+                                                           tiny_batch(1, cfg=FULL, seed=42)])):
+            for bt in batches:
+                la = a.step({k: v.cuda() for k, v in bt.items()})
+                lb = b.step({k: v.cuda() for k, v in bt.items()})
+            torch.cuda.synchronize()
+            same_grad = all(torch.equal(p.grad, q_.grad) for p, q_ in zip(a.params, b.params))
+            same_par = all(torch.equal(p, q_) for p, q_ in zip(a.params, b.params))
+            out[name] = (bool(torch.equal(la, lb)), same_grad, same_par, dict(a.dp.last_buckets))
+        out["backend"] = dist.get_backend()
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_nccl_world1_overlapped_allreduce():
+    """the DP step on RCCL (ProcessGroupNCCL, world size 1, GradAllReduce forced active): the per-
+    stream bucket packing, the async all_reduce on RCCL's stream and finish()'s wait + unpack run for
+    two eager steps, tiny (many 50 KB buckets) and full size (default 32 MB buckets); a one-rank
+    all-reduce is an identity, so losses, gradients and updated parameters equal the trainer
+    without DP bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert out.pop("backend") == "nccl"
+    for name, (same_loss, same_grad, same_par, nb) in out.items():
+        assert same_loss and same_grad and same_par, (name, same_loss, same_grad, same_par)
+        assert len(nb) == 2 and sum(nb.values()) >= 2, (name, nb)  # buckets from both encoder streams
