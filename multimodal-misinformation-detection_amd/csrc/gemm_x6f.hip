@@ -40,17 +40,24 @@ namespace {
 // Diagnostic build only (-DMMFD_XF_STAMPS, tools/xf_stamps.py): s_memtime at the phase boundaries of
 // one mid-loop K-step, per wave, into a buffer no computation reads.
 #ifdef MMFD_XF_STAMPS
-__device__ uint64_t xf_stamps[4096 * 8 * 16];
+__device__ uint64_t xf_stamps[4096 * 8 * 20];
+#define XF_TSTAMP(k)                                                                                  \
+  do {                                                                                                \
+    const uint64_t t__ = __builtin_amdgcn_s_memtime();                                               \
+    const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                                \
+    if (lane == 0 && b__ < 4096) xf_stamps[(b__ * 8 + wave) * 20 + (k)] = t__;                       \
+  } while (0)
 #define XF_STAMP(k)                                                                                   \
   do {                                                                                                \
     if (t == xf_t) {                                                                                  \
       const uint64_t t__ = __builtin_amdgcn_s_memtime();                                             \
       const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                              \
-      if (lane == 0 && b__ < 4096) xf_stamps[(b__ * 8 + wave) * 16 + (k)] = t__;                     \
+      if (lane == 0 && b__ < 4096) xf_stamps[(b__ * 8 + wave) * 20 + (k)] = t__;                     \
     }                                                                                                 \
   } while (0)
 #else
 #define XF_STAMP(k) do { } while (0)
+#define XF_TSTAMP(k) do { } while (0)
 #endif
 
 constexpr int XF_SLOT = 8192;
@@ -118,18 +125,97 @@ __device__ __forceinline__ uint4 xf_frag_b(const char* img, int wc, int j, int l
 // chains' last MFMAs have retired by then: no wait states); scalar v_add_f32 (packed adds beside
 // MFMAs cost more issue cycles), pinned in place by an empty asm so the compiler does not defer
 // them past the phase's barrier
+// XF_DIAG (tools/xf_stamps.py variants only, results wrong by design): 1 = no accumulator adds,
+// 2 = no LDS-DMA refills in the loop, 3 = no fragment reads in the loop
+#ifndef XF_DIAG
+#define XF_DIAG 0
+#endif
 __device__ __forceinline__ void xf_add(f32x4& acc, const f32x4& t) {
+  if (XF_DIAG == 1) {
+    asm volatile("" ::"v"(t));
+    return;
+  }
   acc[0] += t[0]; acc[1] += t[1]; acc[2] += t[2]; acc[3] += t[3];
 }
 #ifndef XF_PRIO_STATIC
 #define XF_PRIO_STATIC 1
 #endif
+#ifndef XF_CHAINS
+#define XF_CHAINS 2
+#endif
+// one (i, j) chain of the six products from zero: mid*mid, hi*lo, lo*hi, hi*mid, mid*hi, hi*hi
+#define XF_P(t, j, i, pb, pa) Mma<bf16>::run(t, b[j][pb], a[i][pa])
 __device__ __forceinline__ void xf_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][3], const uint4 (&b)[2][3]) {
   if (!XF_PRIO_STATIC) __builtin_amdgcn_s_setprio(1);
+#if XF_CHAINS == 4
+  // two A subtiles per group: four independent chains interleaved (an MFMA depends on the one
+  // four slots earlier)
+  f32x4 p[4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    f32x4 t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 1, 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 2, 0);
+    if (g > 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xf_add(acc[c >> 1][c & 1], p[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 0, 2);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 1, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 0, 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) XF_P(t[c], c & 1, 2 * g + (c >> 1), 0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p[c] = t[c];
+    if (g > 0) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xf_add(acc[2 + (c >> 1)][c & 1], p[c]);
+#else
   f32x4 p0, p1;  // the previous subtile's sums
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     f32x4 t0 = f32x4{0.f, 0.f, 0.f, 0.f}, t1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#if XF_CHAINS == 1
+    // one chain after the other: each MFMA depends on the one just before it
+    XF_P(t0, 0, i, 1, 1); XF_P(t0, 0, i, 2, 0);
+    if (i > 0) xf_add(acc[i - 1][0], p0);
+    XF_P(t0, 0, i, 0, 2); XF_P(t0, 0, i, 1, 0); XF_P(t0, 0, i, 0, 1); XF_P(t0, 0, i, 0, 0);
+    XF_P(t1, 1, i, 1, 1); XF_P(t1, 1, i, 2, 0);
+    if (i > 0) xf_add(acc[i - 1][1], p1);
+    XF_P(t1, 1, i, 0, 2); XF_P(t1, 1, i, 1, 0); XF_P(t1, 1, i, 0, 1); XF_P(t1, 1, i, 0, 0);
+    p0 = t0;
+    p1 = t1;
+    if (i > 0) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
+#else
     Mma<bf16>::run(t0, b[0][1], a[i][1]);  // mid * mid
     Mma<bf16>::run(t1, b[1][1], a[i][1]);
     Mma<bf16>::run(t0, b[0][2], a[i][0]);  // A hi * B lo
@@ -159,16 +245,19 @@ __device__ __forceinline__ void xf_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][3
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       }
     }
+#endif
     __builtin_amdgcn_sched_barrier(0);
   }
   xf_add(acc[3][0], p0);
   xf_add(acc[3][1], p1);
+#endif
   // keep every add inside the phase (an input-only use: the compiler may not sink them past the
   // barrier into the next iteration, where the sums would stay live and spill fragments)
   asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]), "v"(acc[2][0]), "v"(acc[2][1]),
                "v"(acc[3][0]), "v"(acc[3][1]));
   if (!XF_PRIO_STATIC) __builtin_amdgcn_s_setprio(0);
 }
+#undef XF_P
 
 // sum of the 3 x 8 bf16 values of one A fragment's planes (hi + mid + lo = the fp32 elements)
 __device__ __forceinline__ float xf_sum3(uint4 h, uint4 m, uint4 l) {
@@ -185,6 +274,7 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  XF_TSTAMP(16);
   const int gx = gridDim.x, gy = gridDim.y;
   // XCD-aware order over the whole grid, split-K index included (see gemm256_kernel)
   const int lt = xcd_remap((blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x, gx * gy * gridDim.z);
@@ -291,12 +381,12 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i][p] = xf_frag_a<TA>(ia + p * XF_SLOT, wr * 4 + i, ln);
+        for (int i = 0; i < 4; ++i) if (XF_DIAG != 3 || t == 0) fa[i][p] = xf_frag_a<TA>(ia + p * XF_SLOT, wr * 4 + i, ln);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
+        for (int j = 0; j < 2; ++j) if (XF_DIAG != 3 || t == 0) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
       }
       if (rs_t) XF_ROWSUM(rs0);
-      if (t + 1 < nk) issue(2, t + 1);
+      if (XF_DIAG != 2 && t + 1 < nk) issue(2, t + 1);
       wait_next(t, false);
       XF_STAMP(1);
       g8_pre_barrier();
@@ -314,8 +404,8 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
-      if (t + 1 < nk) issue(0, t + 1);
+        for (int j = 0; j < 2; ++j) if (XF_DIAG != 3 || t == 0) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
+      if (XF_DIAG != 2 && t + 1 < nk) issue(0, t + 1);
       wait_next(t, false);
       XF_STAMP(5);
       g8_pre_barrier();
@@ -333,9 +423,9 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i][p] = xf_frag_a<TA>(ia + p * XF_SLOT, wr * 4 + i, ln);
+        for (int i = 0; i < 4; ++i) if (XF_DIAG != 3 || t == 0) fa[i][p] = xf_frag_a<TA>(ia + p * XF_SLOT, wr * 4 + i, ln);
       if (rs_t) XF_ROWSUM(rs1);
-      if (t + 1 < nk) issue(3, t + 1);
+      if (XF_DIAG != 2 && t + 1 < nk) issue(3, t + 1);
       wait_next(t, true);
       XF_STAMP(9);
       g8_pre_barrier();
@@ -353,8 +443,8 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
-      if (t + 1 < nk) issue(1, t + 1);
+        for (int j = 0; j < 2; ++j) if (XF_DIAG != 3 || t == 0) fb[j][p] = xf_frag_b<TB>(ib + p * XF_SLOT, wc, j, ln);
+      if (XF_DIAG != 2 && t + 1 < nk) issue(1, t + 1);
       wait_next(t, false);
       XF_STAMP(13);
       g8_pre_barrier();
@@ -369,6 +459,7 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
   if (wr == 0) g8_barrier();  // re-align the wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  XF_TSTAMP(17);
   if (do_rs) {
     rs0 += __shfl_xor(rs0, 16, 64);
     rs0 += __shfl_xor(rs0, 32, 64);
@@ -383,6 +474,10 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
     }
   }
   g8_epilogue<float, false>(acc, smem, e, C, ldc, ws, split, M, N, alpha, m0, n0, tid, lane, wave, wr, wc);
+#ifdef MMFD_XF_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  XF_TSTAMP(18);
+#endif
 #undef XF_ROWSUM
 }
 

@@ -117,6 +117,10 @@ def _worker_full(rank, world, port, q):
         tr.step({k: v.cuda() for k, v in b.items()})
         torch.cuda.synchronize()
         q.put((rank, _grads(tr), dict(dp.last_buckets)))
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -136,7 +140,8 @@ def test_dp_full_size_default_buckets_two_streams():
         p.start()
     res, nb = {}, {}
     for _ in range(world):
-        r, g1, buckets = q.get(timeout=600)
+        r, g1, buckets = q.get(timeout=500)
+        assert buckets is not None, g1  # the worker's traceback
         res[r], nb[r] = g1, buckets
     for p in procs:
         p.join(timeout=120)
@@ -187,11 +192,17 @@ def _worker_nccl(port, q):
                 la = a.step({k: v.cuda() for k, v in bt.items()})
                 lb = b.step({k: v.cuda() for k, v in bt.items()})
             torch.cuda.synchronize()
-            same_grad = all(torch.equal(p.grad, q_.grad) for p, q_ in zip(a.params, b.params))
+            same_grad = all((p.grad is None and q_.grad is None) or
+                            (p.grad is not None and q_.grad is not None and torch.equal(p.grad, q_.grad))
+                            for p, q_ in zip(a.params, b.params))
             same_par = all(torch.equal(p, q_) for p, q_ in zip(a.params, b.params))
             out[name] = (bool(torch.equal(la, lb)), same_grad, same_par, dict(a.dp.last_buckets))
         out["backend"] = dist.get_backend()
         q.put(out)
+    except BaseException:  # report instead of leaving the parent waiting on the queue
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -206,8 +217,9 @@ def test_dp_nccl_world1_overlapped_allreduce():
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
     p.start()
-    out = q.get(timeout=600)
+    out = q.get(timeout=500)
     p.join(timeout=120)
+    assert "error" not in out, out.get("error")
     assert p.exitcode == 0
     assert out.pop("backend") == "nccl"
     for name, (same_loss, same_grad, same_par, nb) in out.items():

@@ -62,14 +62,18 @@ else:
     A = torch.randn(Kd, M, device=dev); B = torch.randn(Kd, N, device=dev); kw = dict(trans_a=True, trans_b=True)
 ap, bp = K.split3(A), K.split3(B)
 out = torch.empty(M, N, device=dev)
+epi = os.environ.get("XF_EPI", "plain")  # plain | gelu (bias + GELU + saved pre-activation, output as planes only)
+if epi == "gelu":
+    kw.update(bias=torch.randn(N, device=dev), act=K.ACT_GELU, aux=torch.empty(M, N, device=dev),
+              out_planes=torch.empty(3, M, N, device=dev, dtype=torch.bfloat16), write_out=False)
 for _ in range(5):
     K.gemm(A, B, out=out, a_planes=ap, b_planes=bp, **kw)
 torch.cuda.synchronize()
 nblk = min(((M + 255) // 256) * ((N + 255) // 256), 4096)
-buf = np.zeros(4096 * 8 * 16, np.uint64)
+buf = np.zeros(4096 * 8 * 20, np.uint64)
 assert lib.mmfd_debug_xf_stamps(buf.ctypes.data, buf.nbytes) == 0
-st = buf.reshape(4096, 8, 16)[:nblk].astype(np.int64)
-print(f"M={M} N={N} K={Kd} {lay}: {nblk} blocks; cycles (median / p90 over blocks), row 0 = waves 0-3, row 1 = 4-7")
+st = buf.reshape(4096, 8, 20)[:nblk].astype(np.int64)
+print(f"M={M} N={N} K={Kd} {lay} epilogue {epi}: {nblk} blocks; cycles (median / p90 over blocks), row 0 = waves 0-3, row 1 = 4-7")
 for row, ws in (("row0", slice(0, 4)), ("row1", slice(4, 8))):
     s = st[:, ws, :]
     for p in range(4):
@@ -86,3 +90,6 @@ for row, ws in (("row0", slice(0, 4)), ("row1", slice(4, 8))):
     tot = s[:, :, 15] - s[:, :, 0]
     print(f"  {row} step (phase 0 start -> phase 3 mfma issued): {np.median(tot):.0f}/{np.percentile(tot, 90):.0f}"
           f"  (ideal: 4 x 768 MFMA cycles x 2 rows = 6144 per step per SIMD)")
+    ml, ep = s[:, :, 17] - s[:, :, 16], s[:, :, 18] - s[:, :, 17]
+    print(f"  {row} tile: main loop {np.median(ml):.0f}/{np.percentile(ml, 90):.0f}, epilogue (stores retired) "
+          f"{np.median(ep):.0f}/{np.percentile(ep, 90):.0f} cycles")
