@@ -188,15 +188,27 @@ def _worker_nccl(port, q):
         for name, a, b, batches in (("tiny", tr_dp, tr_ref, [tiny_batch(4, seed=21), tiny_batch(4, seed=22)]),
                                     ("full", f_dp, f_ref, [tiny_batch(1, cfg=FULL, seed=41),
                                                            tiny_batch(1, cfg=FULL, seed=42)])):
-            for bt in batches:
+            diffs = []
+            for si, bt in enumerate(batches):
                 la = a.step({k: v.cuda() for k, v in bt.items()})
                 lb = b.step({k: v.cuda() for k, v in bt.items()})
-            torch.cuda.synchronize()
-            same_grad = all((p.grad is None and q_.grad is None) or
-                            (p.grad is not None and q_.grad is not None and torch.equal(p.grad, q_.grad))
-                            for p, q_ in zip(a.params, b.params))
-            same_par = all(torch.equal(p, q_) for p, q_ in zip(a.params, b.params))
-            out[name] = (bool(torch.equal(la, lb)), same_grad, same_par, dict(a.dp.last_buckets))
+                torch.cuda.synchronize()
+                names = [n for m in (a.text_encoder, a.image_encoder, a.head) for n, _ in m.named_parameters()]
+                for n, p, q_ in zip(names, a.params, b.params):
+                    if (p.grad is None) != (q_.grad is None):
+                        diffs.append((si, n, "grad None mismatch"))
+                    elif p.grad is not None and not torch.equal(p.grad, q_.grad):
+                        diffs.append((si, n, float((p.grad - q_.grad).abs().max() / p.grad.abs().max())))
+            # bit for bit, except the word-embedding gradient: its scatter-add (misc.hip
+            # embed_word_bwd_kernel) accumulates repeated token ids with fp32 atomics, whose order
+            # is not fixed between runs — 1-ulp differences there (and in those embedding rows after
+            # AdamW) are not a DP effect
+            emb = "embeddings.word_embeddings.weight"
+            same_grad = all(d[1] == emb and isinstance(d[2], float) and d[2] < 1e-6 for d in diffs)
+            same_par = all(torch.equal(p, q_) or (n == emb and float((p - q_).abs().max()) < 1e-6)
+                           for n, p, q_ in zip(names, a.params, b.params))
+            same_loss = bool(torch.equal(la, lb)) or float((la - lb).abs().max()) < 1e-6
+            out[name] = (same_loss, same_grad, same_par, dict(a.dp.last_buckets), diffs[:12])
         out["backend"] = dist.get_backend()
         q.put(out)
     except BaseException:  # report instead of leaving the parent waiting on the queue
@@ -212,7 +224,8 @@ def test_dp_nccl_world1_overlapped_allreduce():
     stream bucket packing, the async all_reduce on RCCL's stream and finish()'s wait + unpack run for
     two eager steps, tiny (many 50 KB buckets) and full size (default 32 MB buckets); a one-rank
     all-reduce is an identity, so losses, gradients and updated parameters equal the trainer
-    without DP bit for bit."""
+    without DP bit for bit (the word-embedding gradient, accumulated with fp32 atomics, within
+    1e-6 of its max)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
@@ -222,6 +235,6 @@ def test_dp_nccl_world1_overlapped_allreduce():
     assert "error" not in out, out.get("error")
     assert p.exitcode == 0
     assert out.pop("backend") == "nccl"
-    for name, (same_loss, same_grad, same_par, nb) in out.items():
-        assert same_loss and same_grad and same_par, (name, same_loss, same_grad, same_par)
+    for name, (same_loss, same_grad, same_par, nb, diffs) in out.items():
+        assert same_loss and same_grad and same_par, (name, same_loss, same_grad, same_par, diffs)
         assert len(nb) == 2 and sum(nb.values()) >= 2, (name, nb)  # buckets from both encoder streams
