@@ -150,17 +150,20 @@ def pmc_traffic(kernel):
     return None, (os.path.basename(files[-1]) if files else None)
 
 
-def extract_main(args, dev, world, rank):
-    """BASELINE config 5: evidence-corpus build — ResNet50 image features (im2im_retrieval.py:29-36)
-    and MPNet CLS text embeddings at L=128 (text2text_retrieval.py:129-157), eval mode, random-init
-    weights, synthetic inputs resident in HBM; each rank processes its own shard (no collective).
-    A step = one batch of `--batch` images + `--batch` texts."""
+GFLOP_RESNET50, GFLOP_MPNET128 = 8.174, 22.35  # per image @224 / per sequence @L=128
+
+
+def extract_leg(args, dev, world, rank, precision):
+    """`--warmup` + `--steps` timed extractor steps of one precision on HBM-resident synthetic
+    inputs (a step = `--batch` images through ResNet50 + `--batch` texts through MPNet at L=128),
+    then the per-GEMM device times of one eager step (GemmProbe) for the roofline line."""
+    from mmfd import kernels as K
     from mmfd.encoders import MPNetConfig, MPNetModel
     from mmfd.evidence import SentenceEncoder, resnet50
 
     torch.manual_seed(42)
-    img = resnet50().to(dev).set_precision(args.precision)
-    enc = SentenceEncoder(MPNetModel(MPNetConfig()), device=dev, precision=args.precision)
+    img = resnet50().to(dev).set_precision(precision)
+    enc = SentenceEncoder(MPNetModel(MPNetConfig()), device=dev, precision=precision)
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     px = torch.randn(args.batch, 3, 224, 224, generator=g).to(dev)
     ids = torch.randint(3, 30527, (args.batch, 128), generator=g)
@@ -199,20 +202,160 @@ def extract_main(args, dev, world, rank):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    items = 2 * args.batch * world * args.steps
+    probe = K.GemmProbe()
+    with probe:
+        step()
+    prof = probe.summary()
+    dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
+    achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    x6 = "x6f_kernel" in dom_name or dom_name.rstrip().endswith("true>")
+    peak = PEAK_TFLOPS[precision] if not x6 else PEAK_TFLOPS["bf16"] / 6
+    traffic, traffic_src = pmc_traffic(dom_name)
+    ips = args.batch * args.steps / (t_img * 1e-3)
+    tps = args.batch * args.steps / (t_txt * 1e-3)
+    step_tf = args.batch * args.steps * (GFLOP_RESNET50 + GFLOP_MPNET128) / ((t_img + t_txt) * 1e-3) / 1e3
+    del img, enc
+    return {"items": 2 * args.batch * world * args.steps / elapsed, "ms": 1000.0 * elapsed / args.steps,
+            "ips": ips, "tps": tps, "step_tflops": step_tf,
+            "roofline": {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 1), "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "launches_per_step": d["launches"], "avg_launch_us": round(1000.0 * d["ms"] / d["launches"], 2),
+                         "algorithmic_flops_per_launch": int(d["flops"] // d["launches"]),
+                         **({"peak_note": "split-operand fp32 ceiling: bf16 dense MFMA peak / 6"} if x6 else {})}}
+
+
+def extract_cpu_baseline(n=4):
+    """the oracle's ResNet50 (oracle/resnet.py) and MPNet (oracle/encoders.py) on `n` images @224 and
+    `n` texts @L=128 on this host's cores (fp32, the reference's own arithmetic)"""
+    from mmfd.encoders import MPNetConfig, MPNetModel
+    from mmfd.evidence import resnet50
+    from oracle import encoders as OE
+    from oracle.resnet import resnet_forward
+    cores = host_cores()
+    torch.set_num_threads(cores)
+    torch.manual_seed(42)
+    P = {k: v.clone() for k, v in resnet50().state_dict().items()}
+    M = {k: v.clone() for k, v in MPNetModel(MPNetConfig()).state_dict().items()}
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, 3, 224, 224, generator=g)
+    ids = torch.randint(3, 30527, (n, 128), generator=g)
+    ids[:, 0] = 0
+    with torch.no_grad():
+        ti = _timed(lambda: resnet_forward(P, x), 2)
+        tt = _timed(lambda: OE.mpnet_forward(P=M, input_ids=ids, attention_mask=torch.ones_like(ids), num_layers=12,
+                                             num_heads=12), 2)
+    return {"value": round(2 * n / (ti + tt), 3), "unit": "items/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/ ResNet50 on {n} images @224 + MPNet on {n} texts @L=128 (fp32 torch, {cores} threads), "
+                      f"1 warmup + 2 timed batches each",
+            "images_per_s": round(n / ti, 3), "texts_per_s": round(n / tt, 3)}
+
+
+def extract_e2e(dev, precision, n_img=1024, n_txt=4096):
+    """config 5 end to end through the product API, from files: `ImageCorpus.create_feature_corpus`
+    over `n_img` JPEG files (375x500, host decode on a thread pool overlapping the GPU, the HIP
+    "retrieval" preprocessing, ResNet50, the reference's pickle corpus written) and
+    `TextCorpus.encode_corpus` over a `{split}_enriched.csv` of `n_txt` texts (a fast word-level
+    tokenizer over a 30,527-entry vocabulary — the hub's MPNet vocabulary is not available offline —
+    length-sorted batches, MPNet, the fp16 embedding store written). Synthetic files in a temp dir."""
+    import tempfile
+
+    import numpy as np
+    import pandas as pd
+    from PIL import Image
+    from tokenizers import Tokenizer, models, pre_tokenizers, processors
+    from transformers import PreTrainedTokenizerFast
+
+    from mmfd.encoders import MPNetConfig, MPNetModel
+    from mmfd.evidence import ImageCorpus, ImageSimilarity, SentenceEncoder, TextCorpus
+    words = [f"w{i}" for i in range(30522)]
+    vocab = {w: i for i, w in enumerate(["<s>", "<pad>", "</s>", "<unk>", "<mask>"] + words)}
+    tk = Tokenizer(models.WordLevel(vocab, unk_token="<unk>"))
+    tk.pre_tokenizer = pre_tokenizers.Whitespace()
+    tk.post_processor = processors.TemplateProcessing(single="<s> $A </s>", special_tokens=[("<s>", 0), ("</s>", 2)])
+    tok = PreTrainedTokenizerFast(tokenizer_object=tk, pad_token="<pad>", unk_token="<unk>", bos_token="<s>",
+                                  eos_token="</s>", mask_token="<mask>")
+    rng = np.random.default_rng(3)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        os.makedirs(os.path.join(d, "imgs"))
+        base = rng.integers(0, 256, (375, 500, 3), dtype=np.uint8)
+        for i in range(n_img):
+            Image.fromarray(np.roll(base, i * 7, axis=1)).save(os.path.join(d, "imgs", f"{i:05d}.jpg"), quality=90)
+        texts = [" ".join(words[j] for j in rng.integers(0, 30522, int(rng.integers(20, 126)))) for _ in range(n_txt)]
+        pd.DataFrame({"id": range(n_txt), "evidence_enriched": texts}).to_csv(os.path.join(d, "train_enriched.csv"),
+                                                                             index=False)
+        torch.manual_seed(42)
+        corpus = ImageCorpus(os.path.join(d, "corpus.pkl"), extractor=ImageSimilarity(device=dev, precision=precision))
+        tc = TextCorpus(d, "train", encoder=SentenceEncoder(MPNetModel(MPNetConfig()), device=dev, precision=precision,
+                                                           tokenizer=tok, max_seq_length=128))
+        warm = os.path.join(d, "warm")  # one small warm-up build (kernel attributes, allocator)
+        os.makedirs(warm)
+        for i in range(8):
+            os.link(os.path.join(d, "imgs", f"{i:05d}.jpg"), os.path.join(warm, f"{i:05d}.jpg"))
+        ImageCorpus(os.path.join(d, "w.pkl"), extractor=corpus.feature_extractor).create_feature_corpus(warm)
+        tc.bi_encoder.encode(texts[:8])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        corpus.create_feature_corpus(os.path.join(d, "imgs"))
+        t1 = time.perf_counter()
+        tc.encode_corpus()
+        t2 = time.perf_counter()
+        assert len(corpus.feature_dict) == n_img
+    return {"images_per_s": round(n_img / (t1 - t0), 1), "texts_per_s": round(n_txt / (t2 - t1), 1),
+            "items_per_s": round((n_img + n_txt) / (t2 - t0), 1), "images": n_img, "texts": n_txt,
+            "note": "ImageCorpus.create_feature_corpus over JPEG files (375x500, host decode on a thread pool "
+                    "overlapping the GPU, HIP preprocessing, ResNet50, pickle corpus written) + "
+                    "TextCorpus.encode_corpus over a CSV (word-level fast tokenizer, length-sorted batches, "
+                    "MPNet, fp16 store written)"}
+
+
+def extract_main(args, dev, world, rank):
+    """BASELINE config 5: evidence-corpus build — ResNet50 image features (im2im_retrieval.py:29-36)
+    and MPNet CLS text embeddings at L=128 (text2text_retrieval.py:129-157), eval mode, random-init
+    weights, fp32 (the reference's precision) with bf16 beside it; the headline times inputs
+    resident in HBM (each rank its own shard, no collective), `e2e` the product API from files."""
+    res = extract_leg(args, dev, world, rank, args.precision)
+    log(f"extract {args.precision}: {res['items']:.1f} items/s")
+    sec = None
+    if args.precision == "fp32" and not args.no_bf16:
+        torch.cuda.empty_cache()
+        sec = extract_leg(args, dev, world, rank, "bf16")
+        log(f"extract bf16: {sec['items']:.1f} items/s")
+    e2e = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            e2e = extract_e2e(dev, args.precision)
+            log(f"extract e2e: {e2e}")
+        except Exception as e:  # never hide the headline
+            e2e = {"error": repr(e)}
     if rank == 0:
-        ips = args.batch * args.steps / (t_img * 1e-3)
-        tps = args.batch * args.steps / (t_txt * 1e-3)
         out = {
             "metric": "evidence-corpus items/sec (ResNet50 image features + MPNet L=128 text embeddings)",
-            "value": round(items / elapsed, 1), "unit": "items/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True,
+            "value": round(res["items"], 1), "unit": "items/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(res["ms"], 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (random-init weights)",
             "config": {"workload": "evidence corpus build (BASELINE config 5): resnet50 @224 + multi-qa-mpnet-base "
                                    "@L=128, eval", "global_batch": args.batch * world, "parallelism": f"shard{world}"},
-            "images_per_s_per_gpu": round(ips, 1), "texts_per_s_per_gpu": round(tps, 1),
-            "image_tflops": round(ips * 8.174e9 / 1e12, 1), "text_tflops": round(tps * 22.35e9 / 1e12, 1),
+            "images_per_s_per_gpu": round(res["ips"], 1), "texts_per_s_per_gpu": round(res["tps"], 1),
+            "image_tflops": round(res["ips"] * GFLOP_RESNET50 / 1e3, 1),
+            "text_tflops": round(res["tps"] * GFLOP_MPNET128 / 1e3, 1),
+            "roofline": res["roofline"],
+            "roofline_step_frac": round(res["step_tflops"] / step_peak(args.precision)[0], 4),
+            "roofline_step_peak": {"peak": round(step_peak(args.precision)[0], 1), "unit": "TFLOP/s",
+                                   "note": step_peak(args.precision)[1] + f"; {GFLOP_RESNET50} GFLOP/image, "
+                                           f"{GFLOP_MPNET128} GFLOP/text (SURVEY 8(d))"},
         }
+        if sec is not None:
+            out["bf16"] = {"value": round(sec["items"], 1), "unit": "items/s",
+                           "images_per_s_per_gpu": round(sec["ips"], 1), "texts_per_s_per_gpu": round(sec["tps"], 1),
+                           "roofline": sec["roofline"]}
+        if e2e is not None:
+            out["e2e"] = e2e
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = extract_cpu_baseline()
+            except Exception as e:
+                out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -616,8 +759,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.precision is None:
-        args.precision = "fp32" if args.workload == "train" else "bf16"
+    if args.precision is None:  # the reference's fp32 for the training step and the corpus build
+        args.precision = "fp32" if args.workload in ("train", "extract") else "bf16"
 
     import mmfd  # noqa: F401
     from mmfd import kernels as K

@@ -258,10 +258,11 @@ def resnet50(**kw):
 # image preprocessing (im2im_retrieval.py:19-27) and the extractor API
 # -------------------------------------------------------------------------------------------------
 def _decode(image):
-    """host decode (PIL) -> RGB PIL image"""
+    """host decode (PIL) -> RGB PIL image (the file is read and closed here)"""
     from PIL import Image
     if not isinstance(image, Image.Image):
-        image = Image.open(image)
+        with Image.open(image) as im:
+            return im.convert("RGB")
     return image.convert("RGB")
 
 
@@ -269,7 +270,9 @@ class ImageSimilarity:
     """im2im_retrieval.py:12-42 — ResNet50 features of one image (`extract_features`) plus the
     batched `extract_batch` the corpus build uses."""
 
-    def __init__(self, state_dict=None, device="cuda", precision="bf16", model=None):
+    def __init__(self, state_dict=None, device="cuda", precision="fp32", model=None):
+        # fp32 by default: the reference extracts in fp32 (im2im_retrieval.py:14-36); "bf16" is the
+        # faster option
         self.model = model if model is not None else resnet50()
         if state_dict is not None:
             self.model.load_state_dict(state_dict, strict=False)
@@ -305,10 +308,14 @@ class ImageCorpus:
     """im2im_retrieval.py:45-78 with batched GPU extraction. The corpus file is the reference's
     pickle (path -> fp32 [2048] tensor) unless its name ends in .npz (`paths`, `features`)."""
 
-    def __init__(self, feature_corpus_path, extractor: ImageSimilarity | None = None, batch_size=256):
+    def __init__(self, feature_corpus_path, extractor: ImageSimilarity | None = None, batch_size=256,
+                 decode_workers=None):
         self.feature_corpus_path = feature_corpus_path
         self.feature_extractor = extractor or ImageSimilarity()
         self.batch_size = batch_size
+        # host decode threads (PIL releases the GIL while it decodes): the next batch is decoded
+        # while the GPU preprocesses and embeds the current one
+        self.decode_workers = decode_workers or min(16, len(os.sched_getaffinity(0)))
         self.feature_dict = self.load_features()
         self._revision = 0  # bumped on every feature_dict write: the device index is rebuilt
 
@@ -344,13 +351,21 @@ class ImageCorpus:
         self.save_features()
 
     def _extract_paths(self, paths):
+        from concurrent.futures import ThreadPoolExecutor
         out = {}
-        for i in range(0, len(paths), self.batch_size):
-            chunk = paths[i:i + self.batch_size]
-            px = self.feature_extractor.preprocess_batch([_decode(p) for p in chunk])
-            feats = self.feature_extractor.extract_batch(px).float().cpu()
-            for p, f in zip(chunk, feats):
-                out[p] = f.clone()
+        chunks = [paths[i:i + self.batch_size] for i in range(0, len(paths), self.batch_size)]
+        if not chunks:
+            return out
+        with ThreadPoolExecutor(max_workers=max(1, self.decode_workers)) as pool:
+            nxt = [pool.submit(_decode, p) for p in chunks[0]]
+            for ci, chunk in enumerate(chunks):
+                imgs = [f.result() for f in nxt]
+                if ci + 1 < len(chunks):  # decode the next batch on the host while this one runs
+                    nxt = [pool.submit(_decode, p) for p in chunks[ci + 1]]
+                px = self.feature_extractor.preprocess_batch(imgs)
+                feats = self.feature_extractor.extract_batch(px).float().cpu()
+                for p, f in zip(chunk, feats):
+                    out[p] = f.clone()
         return out
 
     def create_feature_corpus(self, image_dir, shard=None):
@@ -411,7 +426,7 @@ class SentenceEncoder:
     """MPNet + CLS pooling (SentenceTransformer("multi-qa-mpnet-base-dot-v1").encode semantics on
     token ids). `encode(texts)` needs a tokenizer object (none can be downloaded here)."""
 
-    def __init__(self, model: MPNetModel | None = None, state_dict=None, device="cuda", precision="bf16",
+    def __init__(self, model: MPNetModel | None = None, state_dict=None, device="cuda", precision="fp32",
                  tokenizer=None, max_seq_length=512):
         self.model = model if model is not None else MPNetModel(MPNetConfig())
         if state_dict is not None:
@@ -431,15 +446,36 @@ class SentenceEncoder:
         return torch.cat(outs) if len(outs) > 1 else outs[0]
 
     def encode(self, sentences, batch_size=256, convert_to_tensor=True):
-        """SentenceTransformer.encode: a str gives [768], a list [N, 768] (fp32, host)"""
+        """SentenceTransformer.encode: a str gives [768], a list [N, 768] (fp32, host). As
+        sentence-transformers does, the texts are tokenised once, sorted by length and encoded in
+        batches padded to their own longest text (CLS pooling over masked keys: the padding
+        length does not change an embedding), then returned in input order."""
         if self.tokenizer is None:
             raise RuntimeError("SentenceEncoder.encode needs a tokenizer (pass tokenizer=...); use encode_ids")
         single = isinstance(sentences, str)
-        enc = self.tokenizer([sentences] if single else list(sentences), padding=True, truncation=True,
-                             max_length=self.max_seq_length, return_tensors="pt")
-        emb = self.encode_ids(enc["input_ids"], enc["attention_mask"], batch_size).cpu()
-        emb = emb[0] if single else emb
+        texts = [sentences] if single else list(sentences)
+        if not texts:
+            emb = torch.zeros(0, self.model.config.hidden_size)
+            return emb if convert_to_tensor else emb.numpy()
+        ids = self.tokenizer(texts, truncation=True, max_length=self.max_seq_length)["input_ids"]
+        order = sorted(range(len(ids)), key=lambda i: -len(ids[i]))
+        pad = getattr(self.tokenizer, "pad_token_id", 0) or 0
+        out = torch.empty(len(ids), self.model.config.hidden_size)
+        for i in range(0, len(order), batch_size):
+            idx = order[i:i + batch_size]
+            L = len(ids[idx[0]])
+            x = torch.full((len(idx), L), pad, dtype=torch.int64)
+            m = torch.zeros((len(idx), L), dtype=torch.int64)
+            for r, j in enumerate(idx):
+                x[r, :len(ids[j])] = torch.tensor(ids[j])
+                m[r, :len(ids[j])] = 1
+            dev = self.model_device()
+            out[idx] = self.encode_ids(x.to(dev, non_blocking=True), m.to(dev, non_blocking=True), batch_size).cpu()
+        emb = out[0] if single else out
         return emb if convert_to_tensor else emb.numpy()
+
+    def model_device(self):
+        return next(self.model.parameters()).device
 
 
 class TextCorpus:

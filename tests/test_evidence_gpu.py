@@ -188,3 +188,95 @@ def test_mpnet_base_vs_oracle_l128():
     ref = OE.mpnet_forward(P, ids, mask, num_layers=12, num_heads=12)
     out = m.to(DEV).set_precision("fp32")(input_ids=ids, attention_mask=mask).last_hidden_state
     assert _rel(out, ref) < 1e-3
+
+
+# ---- config 5 sharded over ranks with the HIP extractors (gloo, world 2 on the box's GPU) --------
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _corpus_files(d, n_img=11, n_txt=13):
+    import numpy as np
+    import pandas as pd
+    from PIL import Image
+    rng = np.random.default_rng(2)
+    os.makedirs(os.path.join(d, "imgs"), exist_ok=True)
+    for i in range(n_img):
+        Image.fromarray(rng.integers(0, 256, (180 + 7 * i, 240, 3), dtype=np.uint8)).save(
+            os.path.join(d, "imgs", f"im{i:02d}.jpg"), quality=92)
+    from tests.toy_tokenizer import sentence
+    pd.DataFrame({"id": list(range(n_txt)), "evidence_enriched": [sentence(rng, 3, 60) for _ in range(n_txt)]}).to_csv(
+        os.path.join(d, "train_enriched.csv"), index=False)
+
+
+def _extractors():
+    from mmfd.encoders import MPNetConfig, MPNetModel
+    from mmfd.evidence import ImageSimilarity, SentenceEncoder
+    from tests.toy_tokenizer import toy_tokenizer
+    torch.manual_seed(11)
+    img = ImageSimilarity(model=resnet50(), device=DEV)  # fp32: the reference's precision
+    txt = SentenceEncoder(MPNetModel(MPNetConfig()), device=DEV, tokenizer=toy_tokenizer(), max_seq_length=128)
+    return img, txt
+
+
+def _corpus_worker(rank, world, port, d, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.evidence import ImageCorpus, TextCorpus
+        img, txt = _extractors()
+        ImageCorpus(os.path.join(d, "sharded.pkl"), extractor=img, batch_size=4).create_feature_corpus(
+            os.path.join(d, "imgs"))
+        TextCorpus(d, "train", encoder=txt, out_dir=os.path.join(d, "sharded")).encode_corpus()
+        q.put((rank, None))
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_corpus_build_hip_equals_single_process(tmp_path):
+    """config 5 with the HIP extractors: ResNet50 + MPNet (fp32, random init) over a gloo world of 2
+    ranks on the box's GPU — each rank embeds its contiguous shard of the sorted image files / CSV
+    rows, rank 0 merges — gives the corpus of one process: same paths / ids in the same order,
+    image features within 1e-5 and fp16 text embeddings within 1e-3 of the single-process build
+    (different batch compositions are the only difference)."""
+    import torch.multiprocessing as mp
+    from mmfd.evidence import ImageCorpus, TextCorpus, load_corpus_pickle
+    d = str(tmp_path)
+    _corpus_files(d)
+    os.makedirs(os.path.join(d, "single"))
+    os.makedirs(os.path.join(d, "sharded"))
+    img, txt = _extractors()
+    single = ImageCorpus(os.path.join(d, "single.pkl"), extractor=img, batch_size=5)
+    single.create_feature_corpus(os.path.join(d, "imgs"))
+    one = TextCorpus(d, "train", encoder=txt, out_dir=os.path.join(d, "single")).encode_corpus()
+    del img, txt
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_corpus_worker, args=(r, world, port, d, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        r, err = q.get(timeout=400)
+        assert err is None, err
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    merged = load_corpus_pickle(os.path.join(d, "sharded.pkl"))
+    assert list(merged) == list(single.feature_dict)
+    for k in merged:
+        a, b = merged[k], single.feature_dict[k]
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), k
+    e1, i1 = TextCorpus.read(one)
+    e2, i2 = TextCorpus.read(os.path.join(d, "sharded", os.path.basename(one)))
+    assert i1 == i2 == [f"train_{i}" for i in range(13)]
+    assert np.abs(e1.astype(np.float32) - e2.astype(np.float32)).max() <= 1e-3 * np.abs(e1.astype(np.float32)).max()
