@@ -808,6 +808,7 @@ def main():
                                    "(SURVEY 8(d), algorithmic)"},
             "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
             "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"],
+            "peak_memory_gb": res["peak_memory_gb"],
             "fp32_gemm": ("split operands: x = hi + mid + lo bf16 planes staged together per 32-deep K-step, six bf16 "
                           "MFMA products per fp32 product summed per K-step and added to an fp32 accumulator (error "
                           "0.2-0.4x the fp32 MFMA's, tests/test_kernels_gpu.py; MMFD_FP32_GEMM=native selects the "
@@ -844,6 +845,7 @@ def train_leg(args, dev, world, rank, precision):
 
     graphed = world == 1 and not args.no_graph
     probe = K.GemmProbe()
+    torch.cuda.reset_peak_memory_stats(dev)
     if graphed:  # the whole step as one HIP graph (capture runs its own eager warmup steps first)
         tr.capture(batch, warmup=max(1, args.warmup))
         for _ in range(args.warmup):
@@ -867,6 +869,7 @@ def train_leg(args, dev, world, rank, precision):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 2**30  # the timed step's device memory high-water mark
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -925,7 +928,7 @@ def train_leg(args, dev, world, rank, precision):
                        + ("; text / image encoders on two streams" if tr_conc else "")
                        + "; GEMM times from 2 eager probe steps after the timed region, encoders serialized"),
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
-            "step_peak": step_peak(precision), "roofline": roof}
+            "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1)}
 
 
 def step_peak(precision):

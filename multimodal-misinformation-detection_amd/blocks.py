@@ -433,3 +433,18 @@ def mlp_ln_bwd(ctx: StepCtx, dy2d, st):
     ctx.lin_grads([mlp + w1], dpre, a2d)
     linear_dx(ctx, dpre, mlp + w1, out=ds, beta=1.0)  # da = ds + dpre W1
     return ds
+
+
+def load_state_dict_checked(module, state_dict, benign=("position_ids", "num_batches_tracked")):
+    """module.load_state_dict(strict=False) that fails like strict loading on every missing or
+    unexpected key except the named benign ones (matched as a key suffix or a "prefix." start): a
+    checkpoint whose names do not match must not leave random weights behind plausible outputs"""
+    res = module.load_state_dict(state_dict, strict=False)
+    ok = lambda k: any(k.endswith(b) or k.startswith(b + ".") for b in benign)  # noqa: E731
+    missing = [k for k in res.missing_keys if not ok(k)]
+    unexpected = [k for k in res.unexpected_keys if not ok(k)]
+    if missing or unexpected:
+        raise RuntimeError(f"{type(module).__name__}: state_dict does not match: missing {missing[:8]}"
+                           f"{' ...' if len(missing) > 8 else ''}, unexpected {unexpected[:8]}"
+                           f"{' ...' if len(unexpected) > 8 else ''}")
+    return res

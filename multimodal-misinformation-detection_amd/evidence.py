@@ -33,6 +33,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import blocks as Bk
 from . import kernels as K
 from .encoders import MPNetConfig, MPNetModel
 
@@ -274,8 +275,8 @@ class ImageSimilarity:
         # fp32 by default: the reference extracts in fp32 (im2im_retrieval.py:14-36); "bf16" is the
         # faster option
         self.model = model if model is not None else resnet50()
-        if state_dict is not None:
-            self.model.load_state_dict(state_dict, strict=False)
+        if state_dict is not None:  # a torchvision resnet50 checkpoint: its fc layer is dropped (:14-17)
+            Bk.load_state_dict_checked(self.model, state_dict, benign=("fc", "num_batches_tracked"))
         self.model = self.model.to(device).eval().set_precision(precision)
         self.device = device
         self._pre = None
@@ -429,8 +430,8 @@ class SentenceEncoder:
     def __init__(self, model: MPNetModel | None = None, state_dict=None, device="cuda", precision="fp32",
                  tokenizer=None, max_seq_length=512):
         self.model = model if model is not None else MPNetModel(MPNetConfig())
-        if state_dict is not None:
-            self.model.load_state_dict(state_dict, strict=False)
+        if state_dict is not None:  # sentence-transformers' MPNet checkpoints carry an unused pooler
+            Bk.load_state_dict_checked(self.model, state_dict, benign=("pooler", "position_ids"))
         self.model = self.model.to(device).eval().set_precision(precision)
         self.tokenizer = tokenizer
         self.max_seq_length = max_seq_length

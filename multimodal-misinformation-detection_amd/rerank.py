@@ -81,8 +81,8 @@ class CrossEncoder:
     def __init__(self, model: BertForSequenceClassification | None = None, tokenizer=None, max_length=512,
                  device="cuda", precision="fp32", default_activation="sigmoid", state_dict=None):
         self.model = model if model is not None else BertForSequenceClassification()
-        if state_dict is not None:
-            self.model.load_state_dict(state_dict, strict=False)
+        if state_dict is not None:  # (the tokenizer-side position_ids buffer of HF checkpoints is benign)
+            Bk.load_state_dict_checked(self.model, state_dict)
         self.model = self.model.to(device).eval().set_precision(precision)
         self.tokenizer, self.max_length, self.device = tokenizer, max_length, torch.device(device)
         self.default_activation = default_activation if self.model.num_labels == 1 else None

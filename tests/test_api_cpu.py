@@ -236,3 +236,19 @@ def test_custom_op_boundary_schemas_and_fake_kernels():
         out = torch.empty(10, 24, device="cuda")
         ops.gemm(x.reshape(10, 48), w, False, False, out, 1.0, 0.0, None, None, False, 0, None, 0.0, None, 0, 0,
                  None, 0.0)
+
+
+def test_checked_state_dict_load():
+    """extractor / re-ranker checkpoints load strictly except for named benign keys
+    (blocks.load_state_dict_checked): a mismatched checkpoint raises instead of leaving random
+    weights behind plausible outputs"""
+    import torch.nn as nn
+    from mmfd.blocks import load_state_dict_checked
+    m = nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 2))
+    sd = {k: v.clone() + 1 for k, v in m.state_dict().items()}
+    load_state_dict_checked(m, dict(sd, **{"pooler.dense.weight": torch.zeros(2)}), benign=("pooler",))
+    assert torch.equal(m[0].weight, sd["0.weight"])
+    with pytest.raises(RuntimeError, match="unexpected"):
+        load_state_dict_checked(m, dict(sd, extra=torch.zeros(1)))
+    with pytest.raises(RuntimeError, match="missing"):
+        load_state_dict_checked(m, {k: v for k, v in sd.items() if k != "1.bias"})
