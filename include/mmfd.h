@@ -182,6 +182,13 @@ typedef struct mmfd_attn_args {
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);
 int mmfd_attn_bwd(const mmfd_attn_args* args, mmfd_stream_t stream);
+/* fp32 attention (the reference's SDPA / softmax(QK^T)V in fp32, layers.py:44-56 and the HF encoders'
+   self-attention): mode 1 (default; env MMFD_FP32_ATTN=native, or MMFD_FP32_GEMM=native without it,
+   selects 0 at load) runs every product on split bf16 operands (x = hi + mid + lo, six MFMA products
+   accumulated in fp32, as mmfd_set_fp32_gemm_mode) when D <= 64, D % 8 == 0, there is no relative
+   bias and the resident length (keys; and queries in the backward) is <= 208; mode 0 = the fp32
+   MFMA kernels. Returns the previous mode. */
+int mmfd_set_fp32_attn_mode(int mode);
 
 /* ------------------------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (fusion head nn.LayerNorm model.py:39-46, 155-162, eps 1e-5;     */

@@ -20,6 +20,7 @@
 #include <type_traits>
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -45,6 +46,7 @@ struct AttnP {
   int acc_dq, acc_dkv;
   // fp32 backward: split planes of the packed [dq | dk | dv] buffer (base = dq), see mmfd_attn_args
   bf16* pl; int64_t pl_stride; const float* pl_base; int pl_only;
+  int dbg;  // x6 phase experiments (MMFD_X6A_DBG): 1 = stage zeros, 2 = skip the products
 };
 
 // one fp32 gradient element into the planes at its offset in the packed buffer
@@ -1083,6 +1085,617 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// fp32 attention on split bf16 operands (the fp32 step's attention; mmfd_set_fp32_attn_mode)
+// --------------------------------------------------------------------------------------------
+// gfx950 has no xf32 MFMA and its fp32 MFMA runs at 1/16 of the bf16 rate. As in gemm256_x6f,
+// every fp32 operand is split into three bf16 planes x = hi + mid + lo (the split3 rule; 24
+// significand bits, all of x) and each product accumulates the six plane products
+//   mid*mid, hi*lo, lo*hi, hi*mid, mid*hi, hi*hi
+// on v_mfma_f32_16x16x32_bf16 into fp32 (bf16 x bf16 products are exact; the dropped mid*lo,
+// lo*mid, lo*lo are below 2^-24 relative): 6 x 16 cycles per 16x16x32 fp32 product against
+// 8 x 32 for the fp32 MFMA. Operands resident in LDS (K/V, or Q/dO) are split while they are
+// staged (one fp32 read from HBM, three bf16 plane images of 128-B rows, the bf16 D = 64 swizzle
+// that serves both the row and the ds_read_b64_tr_b16 transposed reads); the per-wave register
+// operands (the wave's own 16 queries or keys) are split once per block, and the softmax-side
+// operands (P, dS) are split in registers right before their products.
+//
+// Geometry (D = 64 images; any D <= 64 with D % 8 == 0, the zero columns skipped by uniform
+// branches): one 8-wave workgroup per (b, h) as the v2 kernels. Two tensors x three planes x
+// L16 rows x 128 B must fit the 160-KB LDS: L16 = L padded to 16 rows <= 208 (BERT L = 128, ViT
+// L = 197). Rows are padded to 16, not to the 32-row k-chunk: the last chunk of a 16-row remainder
+// runs its h = 1 half on a repeat of its h = 0 rows (h1off = 0) against operands that are zero.
+void set_lds_attr(const void* fn, int bytes) {
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+constexpr int X6A_LMAX = 208;
+constexpr int X6A_RB = 128;  // bytes per plane row (64 bf16)
+constexpr int X6A_LDS = 6 * X6A_LMAX * X6A_RB + 3 * X6A_LMAX * 4;
+
+int g_fp32_attn_mode = [] {
+  const char* v = getenv("MMFD_FP32_ATTN");
+  const char* gm = getenv("MMFD_FP32_GEMM");
+  const bool native = (v && (!strcmp(v, "native") || !strcmp(v, "0"))) ||
+                      (!v && gm && (!strcmp(gm, "native") || !strcmp(gm, "0")));
+  return native ? 0 : 1;
+}();
+
+__device__ __forceinline__ void split8(const float* x, uint4& hi, uint4& mid, uint4& lo) {
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const bf16 hu = (bf16)x[u];
+    const float r = x[u] - (float)hu;
+    const bf16 mu = (bf16)r;
+    h[u] = hu;
+    m[u] = mu;
+    l[u] = (bf16)(r - (float)mu);
+  }
+  hi = __builtin_bit_cast(uint4, h);
+  mid = __builtin_bit_cast(uint4, m);
+  lo = __builtin_bit_cast(uint4, l);
+}
+
+// acc += (a0 + a1 + a2) (b0 + b1 + b2) over one 32-deep chunk, planes 0/1/2 = hi/mid/lo, small first
+__device__ __forceinline__ void mma6(f32x4& acc, const uint4& ah, const uint4& am, const uint4& al, const uint4& bh,
+                                     const uint4& bm, const uint4& bl) {
+  Mma<bf16>::run(acc, am, bm);
+  Mma<bf16>::run(acc, ah, bl);
+  Mma<bf16>::run(acc, al, bh);
+  Mma<bf16>::run(acc, ah, bm);
+  Mma<bf16>::run(acc, am, bh);
+  Mma<bf16>::run(acc, ah, bh);
+}
+
+// the planes of 16x16 fp32 accumulators (rows in split order) as the A fragment of one 32-key chunk
+__device__ __forceinline__ void split_acc(const f32x4& a, const f32x4& b, uint4& hi, uint4& mid, uint4& lo) {
+  const float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  split8(x, hi, mid, lo);
+}
+
+// Dropout with 32-bit indices (B*H*Lq*Lk <= 2^32, x6_attn_ok): mmfd_hash_k(key, idx) = mix32(key ^ lo(idx) * C1 ^
+// hi(idx) * C2) with hi(idx) = 0, and lo(idx) * C1 (mod 2^32) advances by additions — C1 per key,
+// Lk * C1 per query — so an element costs one v_add in place of the 64-bit index arithmetic and
+// its two extra 32-bit multiplies (bit-identical masks).
+constexpr uint32_t HASH_C1 = 0x9e3779b1u;
+__device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
+
+// stage the fp32 head slice rows [0, nrows) (zero rows up to nrows_pad) as three plane images; only
+// the D / 8 16-B chunks of a row that the products read are written
+template <int D, int NTH>
+__device__ __forceinline__ void x6_stage(char* img0, int img, const float* __restrict__ base, int64_t st,
+                                         int64_t nrows, int nrows_pad, int tid, int dreal, int dbg) {
+  constexpr int NC = D / 8;
+  for (int c = tid; c < nrows_pad * NC; c += NTH) {
+    const int r = c / NC, ch = c % NC;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (r < nrows && ch * 8 < dreal && !(dbg & 1)) {
+      const float* src = base + (int64_t)r * st + ch * 8;
+      const float4 a = *reinterpret_cast<const float4*>(src);
+      const float4 b = *reinterpret_cast<const float4*>(src + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    }
+    uint4 h, m, l;
+    split8(x, h, m, l);
+    const int off = row_off<bf16, 64>(r, ch);
+    *reinterpret_cast<uint4*>(img0 + off) = h;
+    *reinterpret_cast<uint4*>(img0 + img + off) = m;
+    *reinterpret_cast<uint4*>(img0 + 2 * img + off) = l;
+  }
+}
+
+// one fp32 row's MFMA fragments (lane: elements (kc*4 + g)*8 .. +7) as planes f[plane][kc]
+template <int KCH>
+__device__ __forceinline__ void x6_row_regs(uint4 (&f)[3][KCH], const float* __restrict__ base, int64_t st,
+                                            int64_t row, int64_t nrows, int lane, int dreal) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int kc = 0; kc < KCH; ++kc) {
+    const int col = (kc * 4 + g) * 8;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (row < nrows && col < dreal) {
+      const float* src = base + row * st + col;
+      const float4 a = *reinterpret_cast<const float4*>(src);
+      const float4 b = *reinterpret_cast<const float4*>(src + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    }
+    split8(x, f[0][kc], f[1][kc], f[2][kc]);
+  }
+}
+
+// transposed B fragment of one 32-row chunk c (rows in split order) from a plane image; h1off =
+// byte distance of the chunk's second 16 rows (16 * 128, or 0 to repeat the first half)
+__device__ __forceinline__ uint4 x6_tr_frag(const char* lds, int c, int dsub, int lane, int h1off) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2;
+  const int u = dsub * 4 + (i & 3);
+  const int r = c * 32 + 4 * g + q;
+  const int off = r * X6A_RB + (((u >> 1) ^ (r & 7)) << 4) + ((u & 1) << 3);
+  const uint2 x0 = lds_read_tr16(lds + off);
+  const uint2 x1 = lds_read_tr16(lds + off + h1off);
+  return make_uint4(x0.x, x0.y, x1.x, x1.y);
+}
+
+__device__ __forceinline__ void x6_row_frag3(uint4* f, const char* lds, int img, int sub, int kc, int lane) {
+  f[0] = row_frag<bf16, 64>(lds, sub, kc, lane);
+  f[1] = row_frag<bf16, 64>(lds + img, sub, kc, lane);
+  f[2] = row_frag<bf16, 64>(lds + 2 * img, sub, kc, lane);
+}
+__device__ __forceinline__ void x6_tr_frag3(uint4* f, const char* lds, int img, int c, int d, int lane, int h1off) {
+  f[0] = x6_tr_frag(lds, c, d, lane, h1off);
+  f[1] = x6_tr_frag(lds + img, c, d, lane, h1off);
+  f[2] = x6_tr_frag(lds + 2 * img, c, d, lane, h1off);
+}
+
+// Every product phase below is software pipelined by hand: the fragments of step i + 1 are read
+// (into the other half of a two-deep register buffer) before step i's six MFMAs issue, and the
+// first step of the phase after the softmax is read before the softmax's vector work, so LDS
+// latency hides behind MFMAs instead of stalling each group of six (the compiler-scheduled form
+// read and waited per group: ViT forward 732 us).
+
+template <int D, bool DROP>
+__global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
+  // K/V planes of the head resident; each wave sweeps 16-query blocks with the v2 online softmax
+  constexpr int KCH = D / 32, DT = D / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lk16 = v2_pad(p.Lk, 16);
+  const int img = lk16 * X6A_RB;
+  char* k_img = smem;
+  char* v_img = smem + 3 * img;
+  float* kbias = reinterpret_cast<float*>(smem + 6 * img);
+  x6_stage<D, V2_THREADS>(k_img, img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk,
+                          lk16, tid, p.D, p.dbg);
+  x6_stage<D, V2_THREADS>(v_img, img, reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk,
+                          lk16, tid, p.D, p.dbg);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
+  __syncthreads();
+  const uint64_t seed = DROP ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
+  const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
+  float* ob = reinterpret_cast<float*>(p.o) + b * p.o_sb + h * p.D;
+  const int nqb = (int)((p.Lq + 15) / 16);
+  for (int qbk = (p.dbg & 2) ? nqb : wave; qbk < nqb; qbk += V2_THREADS / 64) {
+    const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
+    uint4 qf[3][KCH];
+    x6_row_regs<KCH>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](int k0, auto nsc) {
+      constexpr int NS = decltype(nsc)::value;  // 16-key subtiles present (4 but in the last chunk)
+      constexpr int NC = (NS + 1) / 2;           // 32-key chunks of P V
+      const char* kc_img = k_img + k0 * X6A_RB;
+      const char* vc_img = v_img + k0 * X6A_RB;
+      f32x4 s[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {  // S^T = K Q^T, steps (kc, ks)
+        constexpr int N = KCH * NS;
+        uint4 f[2][3];
+        x6_row_frag3(f[0], kc_img, img, 0, 0, lane);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          if (i + 1 < N) x6_row_frag3(f[(i + 1) & 1], kc_img, img, (i + 1) % NS, (i + 1) / NS, lane);
+          const int kc = i / NS, ks = i % NS;
+          mma6(s[ks], f[i & 1][0], f[i & 1][1], f[i & 1][2], qf[0][kc], qf[1][kc], qf[2][kc]);
+        }
+      }
+      // P V steps (c, d); an odd last subtile pairs with zero P (s[NS] stays 0) over repeated V rows
+      constexpr int NV = NC * DT;
+      auto ld_v = [&](int i, uint4* f) {
+        const int c = i / DT, d = i % DT;
+        x6_tr_frag3(f, vc_img, img, c, d, lane, (2 * c + 1 < NS) ? 16 * X6A_RB : 0);
+      };
+      uint4 vf[2][3];
+      ld_v(0, vf[0]);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int ks = 0; ks < NS; ++ks) {
+        const float4 kb4 = *reinterpret_cast<const float4*>(kbias + k0 + ks * 16 + 4 * g);
+        const float kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = fmaf(s[ks][r], c2, kb[r]);
+          s[ks][r] = t;
+          mx = fmaxf(mx, t);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NS; ++ks) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(s[ks][r] - mnew);
+          rs += e;
+          s[ks][r] = e;
+        }
+      }
+      if constexpr (DROP) {
+        const uint32_t cc = rowc1 + (uint32_t)k0 * HASH_C1;
+#pragma unroll
+        for (int ks = 0; ks < NS; ++ks)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t hsh = hash_c1(hkey, cc + (uint32_t)(ks * 16 + r) * HASH_C1);
+            s[ks][r] = (hsh < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
+          }
+      }
+      lsum = lsum * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[d][r] *= ar;
+      }
+      uint4 pp[NC][3];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) split_acc(s[2 * c], s[2 * c + 1], pp[c][0], pp[c][1], pp[c][2]);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        if (i + 1 < NV) ld_v(i + 1, vf[(i + 1) & 1]);
+        const int c = i / DT, d = i % DT;
+        mma6(o[d], pp[c][0], pp[c][1], pp[c][2], vf[i & 1][0], vf[i & 1][1], vf[i & 1][2]);
+      }
+    };
+    int k0 = 0;
+    for (; k0 + 64 <= lk16; k0 += 64) chunk(k0, std::integral_constant<int, 4>{});
+    switch ((lk16 - k0) >> 4) {
+      case 1: chunk(k0, std::integral_constant<int, 1>{}); break;
+      case 2: chunk(k0, std::integral_constant<int, 2>{}); break;
+      case 3: chunk(k0, std::integral_constant<int, 3>{}); break;
+      default: break;
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float lr = __shfl(lsum, 4 * g + r, 64);
+      const int64_t q = q0 + 4 * g + r;
+      const float inv = 1.0f / lr;
+      if (q < p.Lq) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          if (d * 16 + li < p.D) {
+            const float val = o[d][r] * inv;
+            ob[q * p.o_st + d * 16 + li] = val;
+            if (p.pl) plane_put(p, ob + q * p.o_st + d * 16 + li, val);
+          }
+      }
+    }
+    if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = (m + log2f(lsum)) * LN2;
+  }
+}
+
+template <int D, bool DROP>
+__global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
+  // Q/dO planes of the head resident (+ lse, delta, key bias); each wave owns 16 keys
+  constexpr int KCH = D / 32, DT = D / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lq16 = v2_pad(p.Lq, 16), lk16 = v2_pad(p.Lk, 16);
+  const int img = lq16 * X6A_RB;
+  char* q_img = smem;
+  char* do_img = smem + 3 * img;
+  float* s_lse = reinterpret_cast<float*>(smem + 6 * img);
+  float* s_delta = s_lse + lq16;
+  float* kbias = s_delta + lq16;
+  x6_stage<D, V2_THREADS>(q_img, img, reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D, p.q_st, p.Lq,
+                          lq16, tid, p.D, p.dbg);
+  x6_stage<D, V2_THREADS>(do_img, img, reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D, p.do_st,
+                          p.Lq, lq16, tid, p.D, p.dbg);
+  for (int i = tid; i < lq16; i += V2_THREADS) {
+    s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] * LOG2E : INFINITY;
+    s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
+  }
+  stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
+  __syncthreads();
+  const float* kb = reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D;
+  const float* vb = reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D;
+  float* dkb = reinterpret_cast<float*>(p.dk) + b * p.dk_sb + h * p.D;
+  float* dvb = reinterpret_cast<float*>(p.dv) + b * p.dv_sb + h * p.D;
+  const uint64_t seed = DROP ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
+  const int nkb = lk16 / 16;
+  for (int kbk = (p.dbg & 2) ? nkb : wave; kbk < nkb; kbk += V2_THREADS / 64) {
+    const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
+    uint4 kf[3][KCH], vf[3][KCH];
+    x6_row_regs<KCH>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
+    x6_row_regs<KCH>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
+    const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
+    const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
+    const uint32_t colc1 = (uint32_t)hcol * HASH_C1 + (uint32_t)(4 * g) * lkc1;
+    f32x4 dkv[2 * DT];  // dV (even) and dK (odd) of each 16-wide D subtile
+#pragma unroll
+    for (int i = 0; i < 2 * DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](int qc, auto nsc) {
+      constexpr int NS = decltype(nsc)::value;  // 16-query subtiles of this 32-query chunk
+      f32x4 sd[4];  // S (even) and dP (odd) per subtile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {  // S = Q K^T and dP = dO V^T, steps (kc, h2)
+        constexpr int N = KCH * NS;
+        uint4 f[2][6];
+        auto ld = [&](int i, uint4* fr) {
+          const int sub = 2 * qc + i % NS, kc = i / NS;
+          x6_row_frag3(fr, q_img, img, sub, kc, lane);
+          x6_row_frag3(fr + 3, do_img, img, sub, kc, lane);
+        };
+        ld(0, f[0]);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          if (i + 1 < N) ld(i + 1, f[(i + 1) & 1]);
+          const int kc = i / NS, h2 = i % NS;
+          const uint4* fr = f[i & 1];
+          mma6(sd[2 * h2], fr[0], fr[1], fr[2], kf[0][kc], kf[1][kc], kf[2][kc]);
+          mma6(sd[2 * h2 + 1], fr[3], fr[4], fr[5], vf[0][kc], vf[1][kc], vf[2][kc]);
+        }
+      }
+      constexpr int h1off = NS == 2 ? 16 * X6A_RB : 0;
+      uint4 tb[2][6];  // transposed dO / Q planes of one D subtile (B operands of dV / dK)
+      auto ldt = [&](int d, uint4* fr) {
+        x6_tr_frag3(fr, do_img, img, qc, d, lane, h1off);
+        x6_tr_frag3(fr + 3, q_img, img, qc, d, lane, h1off);
+      };
+      ldt(0, tb[0]);
+      f32x4 pd[2], ds[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) { pd[h2] = f32x4{0.f, 0.f, 0.f, 0.f}; ds[h2] = pd[h2]; }
+      float z[NS][4];
+#pragma unroll
+      for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
+      if constexpr (DROP) {  // the element index advances by Lk per query
+#pragma unroll
+        for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t e = colc1 + (uint32_t)((2 * qc + h2) * 16 + r) * lkc1;
+            z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
+          }
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < NS; ++h2) {
+        const int qs = 2 * qc + h2;
+        const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
+        const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qs * 16 + 4 * g);
+        const float4 d4 = *reinterpret_cast<const float4*>(s_delta + qs * 16 + 4 * g);
+        const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pr = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, kb2) - lq2[r]);
+          pd[h2][r] = pr * z[h2][r];
+          ds[h2][r] = pr * (dp[r] * z[h2][r] - dl[r]);
+        }
+      }
+      uint4 ph, pm, pl, sh, sm, sl;
+      split_acc(pd[0], pd[1], ph, pm, pl);
+      split_acc(ds[0], ds[1], sh, sm, sl);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        if (d + 1 < DT) ldt(d + 1, tb[(d + 1) & 1]);
+        const uint4* fr = tb[d & 1];
+        mma6(dkv[2 * d], ph, pm, pl, fr[0], fr[1], fr[2]);
+        mma6(dkv[2 * d + 1], sh, sm, sl, fr[3], fr[4], fr[5]);
+      }
+    };
+    const int nfull = lq16 / 32;
+    for (int qc = 0; qc < nfull; ++qc) chunk(qc, std::integral_constant<int, 2>{});
+    if (lq16 & 16) chunk(nfull, std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t key = k0 + 4 * g + r;
+      if (key < p.Lk) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          if (d * 16 + li >= p.D) continue;
+          float* pk = dkb + key * p.dk_st + d * 16 + li;
+          float* pv = dvb + key * p.dv_st + d * 16 + li;
+          float vk = dkv[2 * d + 1][r] * p.scale, vv = dkv[2 * d][r];
+          if (p.acc_dkv) { vk += *pk; vv += *pv; }
+          if (p.pl) {
+            plane_put(p, pk, vk);
+            plane_put(p, pv, vv);
+            if (p.pl_only) continue;
+          }
+          *pk = vk;
+          *pv = vv;
+        }
+      }
+    }
+  }
+}
+
+template <int D, bool DROP>
+__global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
+  // K/V planes of the head resident; each wave owns 16 queries: dQ = dS K
+  constexpr int KCH = D / 32, DT = D / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int lk16 = v2_pad(p.Lk, 16);
+  const int img = lk16 * X6A_RB;
+  char* k_img = smem;
+  char* v_img = smem + 3 * img;
+  float* kbias = reinterpret_cast<float*>(smem + 6 * img);
+  x6_stage<D, V2_THREADS>(k_img, img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk,
+                          lk16, tid, p.D, p.dbg);
+  x6_stage<D, V2_THREADS>(v_img, img, reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk,
+                          lk16, tid, p.D, p.dbg);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
+  __syncthreads();
+  const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
+  const float* dob = reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D;
+  float* dqb = reinterpret_cast<float*>(p.dq) + b * p.dq_sb + h * p.D;
+  const uint64_t seed = DROP ? *p.seed : 0ull;
+  const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const float c2 = p.scale * LOG2E;
+  const int nqb = (int)((p.Lq + 15) / 16);
+  for (int qbk = (p.dbg & 2) ? nqb : wave; qbk < nqb; qbk += V2_THREADS / 64) {
+    const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
+    uint4 qf[3][KCH], dof[3][KCH];
+    x6_row_regs<KCH>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+    x6_row_regs<KCH>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
+    const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
+    const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    f32x4 dq[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](int kc2, auto nsc) {
+      constexpr int NS = decltype(nsc)::value;  // 16-key subtiles of this 32-key chunk
+      f32x4 sd[4];  // S^T (even) and dP^T (odd) per subtile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {  // S^T = K Q^T and dP^T = V dO^T, steps (kc, h2)
+        constexpr int N = KCH * NS;
+        uint4 f[2][6];
+        auto ld = [&](int i, uint4* fr) {
+          const int sub = 2 * kc2 + i % NS, kc = i / NS;
+          x6_row_frag3(fr, k_img, img, sub, kc, lane);
+          x6_row_frag3(fr + 3, v_img, img, sub, kc, lane);
+        };
+        ld(0, f[0]);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          if (i + 1 < N) ld(i + 1, f[(i + 1) & 1]);
+          const int kc = i / NS, h2 = i % NS;
+          const uint4* fr = f[i & 1];
+          mma6(sd[2 * h2], fr[0], fr[1], fr[2], qf[0][kc], qf[1][kc], qf[2][kc]);
+          mma6(sd[2 * h2 + 1], fr[3], fr[4], fr[5], dof[0][kc], dof[1][kc], dof[2][kc]);
+        }
+      }
+      constexpr int h1off = NS == 2 ? 16 * X6A_RB : 0;
+      uint4 tk[2][3];  // transposed K planes of one D subtile (B operand of dQ)
+      x6_tr_frag3(tk[0], k_img, img, kc2, 0, lane, h1off);
+      f32x4 ds[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) ds[h2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float z[NS][4];
+#pragma unroll
+      for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
+      if constexpr (DROP) {
+#pragma unroll
+        for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t e = rowc1 + (uint32_t)((2 * kc2 + h2) * 16 + r) * HASH_C1;
+            z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
+          }
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < NS; ++h2) {
+        const int ks = 2 * kc2 + h2;
+        const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
+        const float4 kb4 = *reinterpret_cast<const float4*>(kbias + ks * 16 + 4 * g);
+        const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pr = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, kbr[r]) - lse2);
+          ds[h2][r] = pr * (dp[r] * z[h2][r] - dlt);
+        }
+      }
+      uint4 sh, sm, sl;
+      split_acc(ds[0], ds[1], sh, sm, sl);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        if (d + 1 < DT) x6_tr_frag3(tk[(d + 1) & 1], k_img, img, kc2, d + 1, lane, h1off);
+        const uint4* fr = tk[d & 1];
+        mma6(dq[d], sh, sm, sl, fr[0], fr[1], fr[2]);
+      }
+    };
+    const int nfull = lk16 / 32;
+    for (int kc2 = 0; kc2 < nfull; ++kc2) chunk(kc2, std::integral_constant<int, 2>{});
+    if (lk16 & 16) chunk(nfull, std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t q = q0 + 4 * g + r;
+      if (q < p.Lq) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          if (d * 16 + li >= p.D) continue;
+          float* pq = dqb + q * p.dq_st + d * 16 + li;
+          float vq = dq[d][r] * p.scale;
+          if (p.acc_dq) vq += *pq;
+          if (p.pl) {
+            plane_put(p, pq, vq);
+            if (p.pl_only) continue;
+          }
+          *pq = vq;
+        }
+      }
+    }
+  }
+}
+
+// the split-operand kernels take this call: fp32, no relative bias, D <= 64 in 16-B-pair chunks,
+// both resident lengths within X6A_LMAX (bwd) / the key length (fwd)
+bool x6_attn_ok(const mmfd_attn_args& a, bool bwd) {
+  if (g_fp32_attn_mode != 1 || a.dtype != MMFD_F32 || a.rel_bias || a.cos_logit_scale) return false;
+  if (a.D % 8 || a.D > 64) return false;
+  if (v2_pad(a.Lk, 16) > X6A_LMAX || (bwd && v2_pad(a.Lq, 16) > X6A_LMAX)) return false;
+  // dropout indices advanced in 32 bits (hash_c1)
+  if (a.dropout_p > 0.f && (uint64_t)a.B * (uint64_t)a.H * (uint64_t)a.Lq * (uint64_t)a.Lk > (1ull << 32)) return false;
+  return !getenv("MMFD_ATTN_V1");
+}
+
+template <int D, bool DROP>
+void launch_fwd_x6_d(const AttnP& p, hipStream_t s) {
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_fwd_x6_kernel<D, DROP>), X6A_LDS), true);
+  (void)once;
+  const int lk16 = v2_pad(p.Lk, 16);
+  hipLaunchKernelGGL((attn_fwd_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+                     6 * lk16 * X6A_RB + lk16 * 4, s, p);
+}
+
+template <int D, bool DROP>
+void launch_bwd_x6_d(const AttnP& p, hipStream_t s) {
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_x6_kernel<D, DROP>), X6A_LDS),
+                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_x6_kernel<D, DROP>), X6A_LDS), true);
+  (void)once;
+  const int64_t rows = p.B * p.H * p.Lq;
+  hipLaunchKernelGGL((attn_delta_kernel<float, D>), dim3((unsigned)((rows * AT<float, D>::NCH + 255) / 256)),
+                     dim3(256), 0, s, p);
+  const int lq16 = v2_pad(p.Lq, 16), lk16 = v2_pad(p.Lk, 16);
+  hipLaunchKernelGGL((attn_dkdv_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+                     6 * lq16 * X6A_RB + (2 * lq16 + lk16) * 4, s, p);
+  hipLaunchKernelGGL((attn_dq_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+                     6 * lk16 * X6A_RB + lk16 * 4, s, p);
+}
+
+// dropout as a template argument: a run-time flag let the compiler if-convert the hash into every
+// chunk (its multiplies issued for dropout-free calls too)
+void launch_fwd_x6(const AttnP& p, hipStream_t s) {
+  const bool dr = p.p > 0.f;
+  if (p.D > 32) { if (dr) launch_fwd_x6_d<64, true>(p, s); else launch_fwd_x6_d<64, false>(p, s); }
+  else { if (dr) launch_fwd_x6_d<32, true>(p, s); else launch_fwd_x6_d<32, false>(p, s); }
+}
+void launch_bwd_x6(const AttnP& p, hipStream_t s) {
+  const bool dr = p.p > 0.f;
+  if (p.D > 32) { if (dr) launch_bwd_x6_d<64, true>(p, s); else launch_bwd_x6_d<64, false>(p, s); }
+  else { if (dr) launch_bwd_x6_d<32, true>(p, s); else launch_bwd_x6_d<32, false>(p, s); }
+}
+
 int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   MMFD_CHECK_ARG(a.dtype == MMFD_F32 || a.dtype == MMFD_BF16, "attn: bad dtype");
   MMFD_CHECK_ARG(a.D > 0 && a.D <= 64, "attn: head_dim %lld unsupported (<= 64)", (long long)a.D);
@@ -1119,11 +1732,9 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.dv = a.dv; p.dv_sb = a.dv_sb; p.dv_st = a.dv_st;
   p.delta = a.delta;
   p.acc_dq = a.accumulate_dq; p.acc_dkv = a.accumulate_dkv;
+  static const int dbg = getenv("MMFD_X6A_DBG") ? atoi(getenv("MMFD_X6A_DBG")) : 0;
+  p.dbg = dbg;
   return 0;
-}
-
-void set_lds_attr(const void* fn, int bytes) {
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 template <typename T, int D, int HPB, bool REL>
@@ -1221,7 +1832,8 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   // batch-1 pair at L = 512 runs faster on the 64-query-block streaming kernel)
   // (fp32 K/V images of 512 keys would not fit the LDS)
   const bool bf = a->dtype == MMFD_BF16;
-  const bool v2 = (p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !getenv("MMFD_ATTN_V1");
+  const bool x6 = x6_attn_ok(*a, false);
+  const bool v2 = x6 || ((p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !getenv("MMFD_ATTN_V1"));
   MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && bf && a->rel_bias),
                  "attn_fwd: cosine attention needs bf16, the resident-K/V kernel (Lk <= 256) and a rel_bias");
   p.pl = nullptr; p.pl_only = 0;
@@ -1231,7 +1843,8 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
                    "attn_fwd: o_planes need an fp32 output in one contiguous [B, Lq, H*D] buffer");
     if (v2) { p.pl = (bf16*)a->o_planes; p.pl_stride = p.B * p.Lq * W; p.pl_base = (const float*)a->o; }
   }
-  if (v2 && bf) { if (a->D > 32) launch_fwd_v2<bf16, 64>(p, s); else launch_fwd_v2<bf16, 32>(p, s); }
+  if (x6) launch_fwd_x6(p, s);
+  else if (v2 && bf) { if (a->D > 32) launch_fwd_v2<bf16, 64>(p, s); else launch_fwd_v2<bf16, 32>(p, s); }
   else if (v2) { if (a->D > 32) launch_fwd_v2<float, 64>(p, s); else launch_fwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
@@ -1248,7 +1861,8 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (rc) return rc;
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const bool v2 = p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1");
+  const bool x6 = x6_attn_ok(*a, true);
+  const bool v2 = x6 || (p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1"));
   p.pl = nullptr; p.pl_only = 0;
   const int64_t W = 3 * a->H * a->D;
   if (a->dqkv_planes) {
@@ -1263,7 +1877,8 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
       p.pl_only = a->planes_only;
     }
   }
-  if (v2 && a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd_v2<bf16, 64>(p, s); else launch_bwd_v2<bf16, 32>(p, s); }
+  if (x6) launch_bwd_x6(p, s);
+  else if (v2 && a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd_v2<bf16, 64>(p, s); else launch_bwd_v2<bf16, 32>(p, s); }
   else if (v2) { if (a->D > 32) launch_bwd_v2<float, 64>(p, s); else launch_bwd_v2<float, 32>(p, s); }
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_bwd<bf16, 64>(p, s); else launch_bwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_bwd<float, 64>(p, s); else launch_bwd<float, 32>(p, s); }
@@ -1271,4 +1886,11 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (a->dqkv_planes && !v2)  // the v1 kernels write fp32 only: split afterwards
     return mmfd_split3(p.B * p.Lq, W, (const float*)a->dq, W, a->dqkv_planes, stream);
   return 0;
+}
+
+extern "C" int mmfd_set_fp32_attn_mode(int mode) {
+  MMFD_CHECK_ARG(mode == 0 || mode == 1, "mmfd_set_fp32_attn_mode: mode %d (0 = fp32 MFMA, 1 = split operands)", mode);
+  const int old = g_fp32_attn_mode;
+  g_fp32_attn_mode = mode;
+  return old;
 }

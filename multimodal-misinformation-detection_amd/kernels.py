@@ -114,6 +114,7 @@ SIGNATURES = {
     "mmfd_gemm": (_I, [ctypes.POINTER(GemmArgs), _VP]),
     "mmfd_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmArgs)]),
     "mmfd_set_fp32_gemm_mode": (_I, [_I]),
+    "mmfd_set_fp32_attn_mode": (_I, [_I]),
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_gemm_runs_split": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
@@ -329,6 +330,15 @@ def set_fp32_gemm_mode(mode):
     old = lib().mmfd_set_fp32_gemm_mode(code)
     _check(0 if old >= 0 else old, "mmfd_set_fp32_gemm_mode")
     _FP32_MODE = code
+    return {0: "native", 1: "split"}[old]
+
+
+def set_fp32_attn_mode(mode):
+    """fp32 attention: 'split' (bf16 operand planes, six MFMA products per product, fp32
+    accumulation; the default) or 'native' (fp32 MFMA). Returns the previous mode name."""
+    code = {"native": 0, "split": 1}[mode]
+    old = lib().mmfd_set_fp32_attn_mode(code)
+    _check(0 if old >= 0 else old, "mmfd_set_fp32_attn_mode")
     return {0: "native", 1: "split"}[old]
 
 

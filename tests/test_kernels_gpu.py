@@ -265,6 +265,53 @@ def test_attention_fwd_bwd(dtype, case, masked, p):
     _close(dv, vr.grad, dtype)
 
 
+@pytest.mark.parametrize("case", [(4, 12, 128, 128, 64, True, 0.1), (3, 12, 197, 197, 64, False, 0.0),
+                                  (2, 8, 128, 197, 32, True, 0.1), (2, 3, 208, 200, 48, True, 0.0),
+                                  (2, 2, 17, 45, 64, False, 0.1)])
+def test_attention_fp32_split_operands_error_matches_fp32_mfma(case):
+    """fp32 attention on split bf16 operands (include/mmfd.h mmfd_set_fp32_attn_mode: every product
+    from the hi/mid/lo planes, six MFMA products accumulated in fp32) against a float64 reference:
+    output, lse and all three gradients may not exceed the fp32-MFMA kernels' own error on the same
+    inputs by more than 1.5x (+1e-7 of the tensor's scale). Covers the encoder shapes (BERT L = 128
+    with mask + dropout, ViT L = 197: an odd 16-row remainder), cross attention at the head's D = 32,
+    D = 48 and the 208-row resident maximum."""
+    B, H, Lq, Lk, D, masked, p = case
+    q = _rand(B, Lq, H * D, seed=30)
+    kv = _rand(B, Lk, 2 * H * D, seed=31)
+    k, v = kv[..., : H * D], kv[..., H * D:]
+    dout = _rand(B, Lq, H * D, seed=32)
+    kb = kb_cpu = None
+    if masked:
+        lens = torch.randint(1, Lk + 1, (B,), generator=torch.Generator().manual_seed(4))
+        mask = (torch.arange(Lk)[None, :] < lens[:, None]).long()
+        kb = K.mask_to_bias(mask.to(DEV))
+        kb_cpu = kb.cpu()
+    seed, salt = K.Seed(78), K.salt_of("test.attn.x6")
+    keep = torch.from_numpy(keep_mask(78, salt, (B, H, Lq, Lk), p)).double() if p > 0 else None
+    qd, kvd, dod = q.to(DEV), kv.to(DEV), dout.to(DEV)
+    outs = {}
+    old = K.set_fp32_attn_mode("split")
+    try:
+        for mode in ("split", "native"):
+            K.set_fp32_attn_mode(mode)
+            o, lse = K.attn_fwd(qd, kvd[..., : H * D], kvd[..., H * D:], H, key_bias=kb, dropout_p=p, seed=seed,
+                                salt=salt)
+            g = K.attn_bwd(qd, kvd[..., : H * D], kvd[..., H * D:], o, lse, dod, H, key_bias=kb, dropout_p=p,
+                           seed=seed, salt=salt)
+            outs[mode] = (o, lse) + tuple(g)
+        torch.cuda.synchronize()
+    finally:
+        K.set_fp32_attn_mode(old)
+    qr, kr, vr = (t.double().requires_grad_(True) for t in (q, k, v))
+    oref, lref = _attn_ref(qr, kr, vr, H, D ** -0.5, kb_cpu, keep, p)
+    oref.backward(dout.double())
+    refs = (oref.detach(), lref, qr.grad, kr.grad, vr.grad)
+    for i, name in enumerate(("o", "lse", "dq", "dk", "dv")):
+        sc = refs[i].abs().max().item()
+        err = {m: (outs[m][i].double().cpu() - refs[i]).abs().max().item() / sc for m in outs}
+        assert err["split"] <= 1.5 * err["native"] + 1e-7, (name, err)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("L", [96, 300])
 def test_attention_batch_strided_rel_bias(dtype, L):

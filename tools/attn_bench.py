@@ -1,6 +1,6 @@
 """Attention kernels at the encoder shapes (bs=256 pairs -> 512 sequences x 12 heads, D=64):
 BERT L=128 with key mask + dropout 0.1, ViT L=197 without. Prints per-kernel-call times.
-python tools/attn_bench.py [--iters N] [--only bert|vit]"""
+python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native]"""
 import argparse
 import os
 import sys
@@ -54,7 +54,9 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--dtype", default="bf16,fp32")
+    ap.add_argument("--fp32-mode", default="split", help="fp32 attention: split (bf16 planes) or native")
     a = ap.parse_args()
+    K.set_fp32_attn_mode(a.fp32_mode)
     for dt in a.dtype.split(","):
         t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
         if a.only in ("", "bert"):
