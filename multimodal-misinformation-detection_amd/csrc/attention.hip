@@ -1109,6 +1109,18 @@ void set_lds_attr(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+// Diagnostic build only (-DMMFD_X6A_STAMPS, tools/x6a_stamps.py): s_memtime per wave at the phase
+// boundaries of the split-operand forward into a buffer no computation reads.
+#ifdef MMFD_X6A_STAMPS
+__device__ uint64_t x6a_stamps[8192 * 8 * 16];
+#define X6A_STAMP(k)                                                                               \
+  do {                                                                                             \
+    const uint64_t t__ = __builtin_amdgcn_s_memtime();                                             \
+    if (lane == 0 && blockIdx.x < 8192) x6a_stamps[((int64_t)blockIdx.x * 8 + wave) * 16 + (k)] = t__; \
+  } while (0)
+#else
+#define X6A_STAMP(k) do { } while (0)
+#endif
 constexpr int X6A_LMAX = 208;
 constexpr int X6A_RB = 128;  // bytes per plane row (64 bf16)
 constexpr int X6A_LDS = 6 * X6A_LMAX * X6A_RB + 3 * X6A_LMAX * 4;
@@ -1161,46 +1173,82 @@ __device__ __forceinline__ void split_acc(const f32x4& a, const f32x4& b, uint4&
 constexpr uint32_t HASH_C1 = 0x9e3779b1u;
 __device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
 
-// stage the fp32 head slice rows [0, nrows) (zero rows up to nrows_pad) as three plane images; only
-// the D / 8 16-B chunks of a row that the products read are written
-template <int D, int NTH>
-__device__ __forceinline__ void x6_stage(char* img0, int img, const float* __restrict__ base, int64_t st,
-                                         int64_t nrows, int nrows_pad, int tid, int dreal, int dbg) {
-  constexpr int NC = D / 8;
-  for (int c = tid; c < nrows_pad * NC; c += NTH) {
-    const int r = c / NC, ch = c % NC;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (r < nrows && ch * 8 < dreal && !(dbg & 1)) {
-      const float* src = base + (int64_t)r * st + ch * 8;
-      const float4 a = *reinterpret_cast<const float4*>(src);
-      const float4 b = *reinterpret_cast<const float4*>(src + 4);
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-    }
-    uint4 h, m, l;
-    split8(x, h, m, l);
-    const int off = row_off<bf16, 64>(r, ch);
-    *reinterpret_cast<uint4*>(img0 + off) = h;
-    *reinterpret_cast<uint4*>(img0 + img + off) = m;
-    *reinterpret_cast<uint4*>(img0 + 2 * img + off) = l;
-  }
-}
-
-// one fp32 row's MFMA fragments (lane: elements (kc*4 + g)*8 .. +7) as planes f[plane][kc]
+// one fp32 row's MFMA fragments (lane: elements (kc*4 + g)*8 .. +7): loaded raw, split into planes
+// f[plane][kc] later (the loads of the next block issue before the current block's products)
+template <int KCH> struct X6Row { float4 v[KCH][2]; };
 template <int KCH>
-__device__ __forceinline__ void x6_row_regs(uint4 (&f)[3][KCH], const float* __restrict__ base, int64_t st,
-                                            int64_t row, int64_t nrows, int lane, int dreal) {
+__device__ __forceinline__ void x6_row_load(X6Row<KCH>& x, const float* __restrict__ base, int64_t st, int64_t row,
+                                            int64_t nrows, int lane, int dreal) {
   const int g = lane >> 4;
 #pragma unroll
   for (int kc = 0; kc < KCH; ++kc) {
     const int col = (kc * 4 + g) * 8;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    x.v[kc][0] = x.v[kc][1] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row < nrows && col < dreal) {
       const float* src = base + row * st + col;
-      const float4 a = *reinterpret_cast<const float4*>(src);
-      const float4 b = *reinterpret_cast<const float4*>(src + 4);
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      x.v[kc][0] = *reinterpret_cast<const float4*>(src);
+      x.v[kc][1] = *reinterpret_cast<const float4*>(src + 4);
     }
-    split8(x, f[0][kc], f[1][kc], f[2][kc]);
+  }
+}
+template <int KCH>
+__device__ __forceinline__ void x6_row_split(uint4 (&f)[3][KCH], const X6Row<KCH>& x) {
+#pragma unroll
+  for (int kc = 0; kc < KCH; ++kc) {
+    const float4 a = x.v[kc][0], b = x.v[kc][1];
+    const float e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    split8(e, f[0][kc], f[1][kc], f[2][kc]);
+  }
+}
+
+// stage two fp32 head slices (rows [0, nrows), zero rows up to nrows_pad) as three plane images
+// each: every load of the thread is issued before the first split, so the HBM latency is paid once
+// per workgroup rather than once per 16-B chunk (the one-chunk-at-a-time loop took ~16k cycles
+// for a 197-row K|V pair, 26 % of the ViT forward workgroup)
+template <int D, int NTH>
+__device__ __forceinline__ void x6_stage2(char* img_a, const float* __restrict__ base_a, int64_t st_a, char* img_b,
+                                          const float* __restrict__ base_b, int64_t st_b, int img, int64_t nrows,
+                                          int nrows_pad, int tid, int dreal, int dbg) {
+  constexpr int NC = D / 8;
+  constexpr int MAXT = (X6A_LMAX * NC + NTH - 1) / NTH;
+  const int total = nrows_pad * NC;
+  float4 xa[MAXT][2], xb[MAXT][2];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int c = tid + j * NTH;
+    const int r = c / NC, ch = c % NC;
+    xa[j][0] = xa[j][1] = xb[j][0] = xb[j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < total && r < nrows && ch * 8 < dreal && !(dbg & 1)) {
+      const float* sa = base_a + (int64_t)r * st_a + ch * 8;
+      const float* sb = base_b + (int64_t)r * st_b + ch * 8;
+      xa[j][0] = *reinterpret_cast<const float4*>(sa);
+      xa[j][1] = *reinterpret_cast<const float4*>(sa + 4);
+      xb[j][0] = *reinterpret_cast<const float4*>(sb);
+      xb[j][1] = *reinterpret_cast<const float4*>(sb + 4);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int c = tid + j * NTH;
+    if (c < total) {
+      const int r = c / NC, ch = c % NC;
+      const int off = row_off<bf16, 64>(r, ch);
+      uint4 h, m, l;
+      {
+        const float e[8] = {xa[j][0].x, xa[j][0].y, xa[j][0].z, xa[j][0].w, xa[j][1].x, xa[j][1].y, xa[j][1].z, xa[j][1].w};
+        split8(e, h, m, l);
+        *reinterpret_cast<uint4*>(img_a + off) = h;
+        *reinterpret_cast<uint4*>(img_a + img + off) = m;
+        *reinterpret_cast<uint4*>(img_a + 2 * img + off) = l;
+      }
+      {
+        const float e[8] = {xb[j][0].x, xb[j][0].y, xb[j][0].z, xb[j][0].w, xb[j][1].x, xb[j][1].y, xb[j][1].z, xb[j][1].w};
+        split8(e, h, m, l);
+        *reinterpret_cast<uint4*>(img_b + off) = h;
+        *reinterpret_cast<uint4*>(img_b + img + off) = m;
+        *reinterpret_cast<uint4*>(img_b + 2 * img + off) = l;
+      }
+    }
   }
 }
 
@@ -1241,27 +1289,32 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  X6A_STAMP(0);
   const int lk16 = v2_pad(p.Lk, 16);
   const int img = lk16 * X6A_RB;
   char* k_img = smem;
   char* v_img = smem + 3 * img;
   float* kbias = reinterpret_cast<float*>(smem + 6 * img);
-  x6_stage<D, V2_THREADS>(k_img, img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk,
-                          lk16, tid, p.D, p.dbg);
-  x6_stage<D, V2_THREADS>(v_img, img, reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk,
-                          lk16, tid, p.D, p.dbg);
+  const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
+  X6Row<KCH> qn;  // the wave's next query block, raw (one block ahead)
+  x6_row_load<KCH>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+  x6_stage2<D, V2_THREADS>(k_img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, v_img,
+                           reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, img, p.Lk, lk16, tid,
+                           p.D, p.dbg);
   stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
   __syncthreads();
+  X6A_STAMP(1);
   const uint64_t seed = DROP ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
-  const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
   float* ob = reinterpret_cast<float*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
   for (int qbk = (p.dbg & 2) ? nqb : wave; qbk < nqb; qbk += V2_THREADS / 64) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[3][KCH];
-    x6_row_regs<KCH>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+    x6_row_split<KCH>(qf, qn);
+    if (qbk + V2_THREADS / 64 < nqb) x6_row_load<KCH>(qn, qb, p.q_st, myq + V2_THREADS / 4, p.Lq, lane, p.D);
+    if (qbk == wave) X6A_STAMP(2);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
     float m = -INFINITY, lsum = 0.f;
@@ -1350,13 +1403,17 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
       }
     };
     int k0 = 0;
-    for (; k0 + 64 <= lk16; k0 += 64) chunk(k0, std::integral_constant<int, 4>{});
+    for (; k0 + 64 <= lk16; k0 += 64) {
+      chunk(k0, std::integral_constant<int, 4>{});
+      if (qbk == wave && k0 < 256) X6A_STAMP(3 + k0 / 64);
+    }
     switch ((lk16 - k0) >> 4) {
       case 1: chunk(k0, std::integral_constant<int, 1>{}); break;
       case 2: chunk(k0, std::integral_constant<int, 2>{}); break;
       case 3: chunk(k0, std::integral_constant<int, 3>{}); break;
       default: break;
     }
+    if (qbk == wave) X6A_STAMP(7);
     lsum += __shfl_xor(lsum, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
 #pragma unroll
@@ -1375,7 +1432,9 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
       }
     }
     if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = (m + log2f(lsum)) * LN2;
+    if (qbk == wave) X6A_STAMP(8);
   }
+  X6A_STAMP(9);
 }
 
 template <int D, bool DROP>
@@ -1393,29 +1452,33 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   float* s_lse = reinterpret_cast<float*>(smem + 6 * img);
   float* s_delta = s_lse + lq16;
   float* kbias = s_delta + lq16;
-  x6_stage<D, V2_THREADS>(q_img, img, reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D, p.q_st, p.Lq,
-                          lq16, tid, p.D, p.dbg);
-  x6_stage<D, V2_THREADS>(do_img, img, reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D, p.do_st,
-                          p.Lq, lq16, tid, p.D, p.dbg);
+  const float* kb = reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D;
+  const float* vb = reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D;
+  X6Row<KCH> kn, vn;  // the wave's first key block, raw (loaded with the staging)
+  x6_row_load<KCH>(kn, kb, p.k_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
+  x6_row_load<KCH>(vn, vb, p.v_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
+  x6_stage2<D, V2_THREADS>(q_img, reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D, p.q_st, do_img,
+                           reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D, p.do_st, img, p.Lq, lq16,
+                           tid, p.D, p.dbg);
   for (int i = tid; i < lq16; i += V2_THREADS) {
     s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] * LOG2E : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
   }
   stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
   __syncthreads();
-  const float* kb = reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D;
-  const float* vb = reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D;
   float* dkb = reinterpret_cast<float*>(p.dk) + b * p.dk_sb + h * p.D;
   float* dvb = reinterpret_cast<float*>(p.dv) + b * p.dv_sb + h * p.D;
   const uint64_t seed = DROP ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
   const int nkb = lk16 / 16;
-  for (int kbk = (p.dbg & 2) ? nkb : wave; kbk < nkb; kbk += V2_THREADS / 64) {
+  // one key block; called for the first block on the rows loaded with the staging and then on
+  // fresh loads (a loop over both would keep the prefetched rows live across the back edge)
+  auto kblock = [&](int kbk, const X6Row<KCH>& kr, const X6Row<KCH>& vr) {
     const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
     uint4 kf[3][KCH], vf[3][KCH];
-    x6_row_regs<KCH>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
-    x6_row_regs<KCH>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    x6_row_split<KCH>(kf, kr);
+    x6_row_split<KCH>(vf, vr);
     const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
     const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
@@ -1519,6 +1582,14 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
         }
       }
     }
+  };
+  if (p.dbg & 2) return;
+  if (wave < nkb) kblock(wave, kn, vn);
+  for (int kbk = wave + V2_THREADS / 64; kbk < nkb; kbk += V2_THREADS / 64) {
+    X6Row<KCH> kr, vr;
+    x6_row_load<KCH>(kr, kb, p.k_st, (int64_t)kbk * 16 + li, p.Lk, lane, p.D);
+    x6_row_load<KCH>(vr, vb, p.v_st, (int64_t)kbk * 16 + li, p.Lk, lane, p.D);
+    kblock(kbk, kr, vr);
   }
 }
 
@@ -1535,24 +1606,26 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   char* k_img = smem;
   char* v_img = smem + 3 * img;
   float* kbias = reinterpret_cast<float*>(smem + 6 * img);
-  x6_stage<D, V2_THREADS>(k_img, img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, p.Lk,
-                          lk16, tid, p.D, p.dbg);
-  x6_stage<D, V2_THREADS>(v_img, img, reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk,
-                          lk16, tid, p.D, p.dbg);
-  stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
-  __syncthreads();
   const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
   const float* dob = reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D;
+  X6Row<KCH> qn, don;  // the wave's first query block, raw (loaded with the staging)
+  x6_row_load<KCH>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+  x6_row_load<KCH>(don, dob, p.do_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+  x6_stage2<D, V2_THREADS>(k_img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, v_img,
+                           reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, img, p.Lk, lk16, tid,
+                           p.D, p.dbg);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk16, tid);
+  __syncthreads();
   float* dqb = reinterpret_cast<float*>(p.dq) + b * p.dq_sb + h * p.D;
   const uint64_t seed = DROP ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
-  for (int qbk = (p.dbg & 2) ? nqb : wave; qbk < nqb; qbk += V2_THREADS / 64) {
+  auto qblock = [&](int qbk, const X6Row<KCH>& qr, const X6Row<KCH>& dr) {  // as kblock in dK/dV
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[3][KCH], dof[3][KCH];
-    x6_row_regs<KCH>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
-    x6_row_regs<KCH>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
+    x6_row_split<KCH>(qf, qr);
+    x6_row_split<KCH>(dof, dr);
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
     const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
@@ -1645,6 +1718,14 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
         }
       }
     }
+  };
+  if (p.dbg & 2) return;
+  if (wave < nqb) qblock(wave, qn, don);
+  for (int qbk = wave + V2_THREADS / 64; qbk < nqb; qbk += V2_THREADS / 64) {
+    X6Row<KCH> qr, dr;
+    x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
+    x6_row_load<KCH>(dr, dob, p.do_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
+    qblock(qbk, qr, dr);
   }
 }
 
@@ -1894,3 +1975,9 @@ extern "C" int mmfd_set_fp32_attn_mode(int mode) {
   g_fp32_attn_mode = mode;
   return old;
 }
+
+#ifdef MMFD_X6A_STAMPS
+extern "C" int mmfd_debug_x6a_stamps(void* host_dst, int64_t bytes) {
+  return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(x6a_stamps), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

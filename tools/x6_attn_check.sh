@@ -8,3 +8,6 @@ echo TESTS_OK; tail -3 gpurun_out/x6a_t.log
 timeout -k 10 200 python -u tools/attn_bench.py --dtype fp32 --fp32-mode split > gpurun_out/x6a_b.log 2>&1 &&
 timeout -k 10 200 python -u tools/attn_bench.py --dtype fp32,bf16 --fp32-mode native >> gpurun_out/x6a_b.log 2>&1
 cat gpurun_out/x6a_b.log
+if [ -f tools/_stamps/libmmfd_hip_x6astamps.so ] && [ "${STAMPS:-0}" = 1 ]; then
+  timeout -k 10 120 python tools/x6a_stamps.py vit && timeout -k 10 120 python tools/x6a_stamps.py bert
+fi
