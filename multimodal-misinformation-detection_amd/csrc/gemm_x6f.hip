@@ -141,13 +141,28 @@ __device__ __forceinline__ void xf_add(f32x4& acc, const f32x4& t) {
 #define XF_PRIO_STATIC 1
 #endif
 #ifndef XF_CHAINS
-#define XF_CHAINS 2
+#define XF_CHAINS 0
 #endif
 // one (i, j) chain of the six products from zero: mid*mid, hi*lo, lo*hi, hi*mid, mid*hi, hi*hi
 #define XF_P(t, j, i, pb, pa) Mma<bf16>::run(t, b[j][pb], a[i][pa])
 __device__ __forceinline__ void xf_mma(f32x4 (&acc)[4][2], const uint4 (&a)[4][3], const uint4 (&b)[2][3]) {
   if (!XF_PRIO_STATIC) __builtin_amdgcn_s_setprio(1);
-#if XF_CHAINS == 4
+#if XF_CHAINS == 0
+  // the six products straight into the fp32 accumulators, small first per K-step, the two B
+  // subtiles' chains interleaved. tools/mb/mfma_rate.hip (one wave per SIMD, this phase's 48
+  // MFMAs): 16.4 cycles per MFMA, against 19.6 for the partial-sum chains from zero plus one
+  // accumulator add each (the adds wait on their chain's last MFMA). Rounding: six adds at the
+  // accumulator's scale per 32-deep K-step, where the fp32 MFMA takes eight (16x16x4 steps)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    XF_P(acc[i][0], 0, i, 1, 1); XF_P(acc[i][1], 1, i, 1, 1);  // mid * mid
+    XF_P(acc[i][0], 0, i, 2, 0); XF_P(acc[i][1], 1, i, 2, 0);  // A hi * B lo
+    XF_P(acc[i][0], 0, i, 0, 2); XF_P(acc[i][1], 1, i, 0, 2);  // A lo * B hi
+    XF_P(acc[i][0], 0, i, 1, 0); XF_P(acc[i][1], 1, i, 1, 0);  // A hi * B mid
+    XF_P(acc[i][0], 0, i, 0, 1); XF_P(acc[i][1], 1, i, 0, 1);  // A mid * B hi
+    XF_P(acc[i][0], 0, i, 0, 0); XF_P(acc[i][1], 1, i, 0, 0);  // hi * hi
+  }
+#elif XF_CHAINS == 4
   // two A subtiles per group: four independent chains interleaved (an MFMA depends on the one
   // four slots earlier)
   f32x4 p[4];
