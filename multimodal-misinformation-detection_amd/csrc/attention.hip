@@ -1309,18 +1309,13 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
   const float c2 = p.scale * LOG2E;
   float* ob = reinterpret_cast<float*>(p.o) + b * p.o_sb + h * p.D;
   const int nqb = (int)((p.Lq + 15) / 16);
-  for (int qbk = (p.dbg & 2) ? nqb : wave; qbk < nqb; qbk += V2_THREADS / 64) {
+  // one query block over the 64-key chunks [c0, c1) (online softmax state o, m, lsum)
+  const int nfc = lk16 / 64;                       // full 64-key chunks
+  const int nchk = nfc + ((lk16 & 63) ? 1 : 0);    // + the padded tail chunk
+  auto qrun = [&](int qbk, const uint4 (&qf)[3][KCH], int c0, int c1, f32x4 (&o)[DT], float& m, float& lsum) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
-    uint4 qf[3][KCH];
-    x6_row_split<KCH>(qf, qn);
-    if (qbk + V2_THREADS / 64 < nqb) x6_row_load<KCH>(qn, qb, p.q_st, myq + V2_THREADS / 4, p.Lq, lane, p.D);
-    if (qbk == wave) X6A_STAMP(2);
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
-    float m = -INFINITY, lsum = 0.f;
-    f32x4 o[DT];
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto chunk = [&](int k0, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-key subtiles present (4 but in the last chunk)
       constexpr int NC = (NS + 1) / 2;           // 32-key chunks of P V
@@ -1402,20 +1397,21 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
         mma6(o[d], pp[c][0], pp[c][1], pp[c][2], vf[i & 1][0], vf[i & 1][1], vf[i & 1][2]);
       }
     };
-    int k0 = 0;
-    for (; k0 + 64 <= lk16; k0 += 64) {
-      chunk(k0, std::integral_constant<int, 4>{});
-      if (qbk == wave && k0 < 256) X6A_STAMP(3 + k0 / 64);
+    const int ce = c1 < nfc ? c1 : nfc;
+    for (int c = c0; c < ce; ++c) chunk(c * 64, std::integral_constant<int, 4>{});
+    if (c1 > nfc) {
+      const int k0 = nfc * 64;
+      switch ((lk16 - k0) >> 4) {
+        case 1: chunk(k0, std::integral_constant<int, 1>{}); break;
+        case 2: chunk(k0, std::integral_constant<int, 2>{}); break;
+        case 3: chunk(k0, std::integral_constant<int, 3>{}); break;
+        default: break;
+      }
     }
-    switch ((lk16 - k0) >> 4) {
-      case 1: chunk(k0, std::integral_constant<int, 1>{}); break;
-      case 2: chunk(k0, std::integral_constant<int, 2>{}); break;
-      case 3: chunk(k0, std::integral_constant<int, 3>{}); break;
-      default: break;
-    }
-    if (qbk == wave) X6A_STAMP(7);
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
+  };
+  // normalise and store one query block (lsum already summed over the four lane groups)
+  auto qfin = [&](int qbk, const f32x4 (&o)[DT], float m, float lsum) {
+    const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float lr = __shfl(lsum, 4 * g + r, 64);
@@ -1432,7 +1428,68 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
       }
     }
     if (g == 0 && myq < p.Lq) p.lse[bh * p.Lq + myq] = (m + log2f(lsum)) * LN2;
+  };
+  if (p.dbg & 2) return;
+  // the last query block halved over the key chunks between two SIMD pairs when the blocks do not
+  // spread evenly (ViT: 13 blocks), as in dK/dV; the halves' softmax states merge in LDS
+  const int R = nqb - V2_THREADS / 64;
+  const bool split = R >= 1 && R <= V2_THREADS / 64 && (R & 3) == 1 && nchk >= 2;
+  const int nwhole = split ? nqb - 1 : nqb;
+  for (int qbk = wave; qbk < nwhole; qbk += V2_THREADS / 64) {
+    uint4 qf[3][KCH];
+    x6_row_split<KCH>(qf, qn);
+    if (qbk + V2_THREADS / 64 < nwhole)
+      x6_row_load<KCH>(qn, qb, p.q_st, (int64_t)(qbk + V2_THREADS / 64) * 16 + li, p.Lq, lane, p.D);
+    if (qbk == wave) X6A_STAMP(2);
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    qrun(qbk, qf, 0, nchk, o, m, lsum);
+    if (qbk == wave) X6A_STAMP(7);
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    qfin(qbk, o, m, lsum);
     if (qbk == wave) X6A_STAMP(8);
+  }
+  if (split) {
+    const int sb = nqb - 1, hc = nchk / 2;
+    const bool own = wave == R - 1, part = wave == R;
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (own || part) {
+      X6Row<KCH> qr;
+      x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
+      uint4 qf[3][KCH];
+      x6_row_split<KCH>(qf, qr);
+      qrun(sb, qf, own ? 0 : hc, own ? hc : nchk, o, m, lsum);
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+    }
+    __syncthreads();  // every wave is done with the K / V images: reuse them for the exchange
+    f32x4* xo = reinterpret_cast<f32x4*>(smem);
+    float* xm = reinterpret_cast<float*>(smem + DT * 64 * 16);
+    if (part) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) xo[d * 64 + lane] = o[d];
+      xm[lane] = m;
+      xm[64 + lane] = lsum;
+    }
+    __syncthreads();
+    if (own) {  // merge: m = max, each half's sums rescaled by exp2(m_half - m)
+      const float mb = xm[lane], lb = xm[64 + lane];
+      const float mm = fmaxf(m, mb);
+      const float aa = __builtin_amdgcn_exp2f(m - mm), ab = __builtin_amdgcn_exp2f(mb - mm);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ra = __shfl(aa, 4 * g + r, 64), rb = __shfl(ab, 4 * g + r, 64);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[d][r] = o[d][r] * ra + xo[d * 64 + lane][r] * rb;
+      }
+      qfin(sb, o, mm, lsum * aa + lb * ab);
+    }
   }
   X6A_STAMP(9);
 }
@@ -1474,7 +1531,9 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   const int nkb = lk16 / 16;
   // one key block; called for the first block on the rows loaded with the staging and then on
   // fresh loads (a loop over both would keep the prefetched rows live across the back edge)
-  auto kblock = [&](int kbk, const X6Row<KCH>& kr, const X6Row<KCH>& vr) {
+  // dK / dV of one key block over the query chunks [qa, qb) into dkv (dV even, dK odd per 16-wide
+  // D subtile)
+  auto kblock = [&](int kbk, const X6Row<KCH>& kr, const X6Row<KCH>& vr, int qa, int qb, f32x4 (&dkv)[2 * DT]) {
     const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
     uint4 kf[3][KCH], vf[3][KCH];
     x6_row_split<KCH>(kf, kr);
@@ -1483,9 +1542,6 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
     const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
     const uint32_t colc1 = (uint32_t)hcol * HASH_C1 + (uint32_t)(4 * g) * lkc1;
-    f32x4 dkv[2 * DT];  // dV (even) and dK (odd) of each 16-wide D subtile
-#pragma unroll
-    for (int i = 0; i < 2 * DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto chunk = [&](int qc, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-query subtiles of this 32-query chunk
       f32x4 sd[4];  // S (even) and dP (odd) per subtile
@@ -1559,8 +1615,12 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
       }
     };
     const int nfull = lq16 / 32;
-    for (int qc = 0; qc < nfull; ++qc) chunk(qc, std::integral_constant<int, 2>{});
-    if (lq16 & 16) chunk(nfull, std::integral_constant<int, 1>{});
+    const int qe = qb < nfull ? qb : nfull;
+    for (int qc = qa; qc < qe; ++qc) chunk(qc, std::integral_constant<int, 2>{});
+    if (qb > nfull) chunk(nfull, std::integral_constant<int, 1>{});
+  };
+  auto kstore = [&](int kbk, const f32x4 (&dkv)[2 * DT]) {
+    const int64_t k0 = (int64_t)kbk * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t key = k0 + 4 * g + r;
@@ -1584,12 +1644,55 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
     }
   };
   if (p.dbg & 2) return;
-  if (wave < nkb) kblock(wave, kn, vn);
-  for (int kbk = wave + V2_THREADS / 64; kbk < nkb; kbk += V2_THREADS / 64) {
+  // 8 waves share the key blocks round robin; waves w and w + 4 share a SIMD, so with R = nkb - 8
+  // extra blocks and R % 4 == 1 (ViT: 13 blocks) one SIMD pair would carry one block more than the
+  // others. The last block is then halved over the query chunks between waves R - 1 and R (two
+  // SIMD pairs), whose partial sums meet in LDS once every wave is done with the Q / dO images.
+  const int nch = lq16 / 32 + ((lq16 & 16) ? 1 : 0);
+  const int R = nkb - V2_THREADS / 64;
+  const bool split = R >= 1 && R <= V2_THREADS / 64 && (R & 3) == 1 && nch >= 2;
+  const int nwhole = split ? nkb - 1 : nkb;
+  if (wave < nwhole) {
+    f32x4 dkv[2 * DT];
+#pragma unroll
+    for (int i = 0; i < 2 * DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kblock(wave, kn, vn, 0, nch, dkv);
+    kstore(wave, dkv);
+  }
+  for (int kbk = wave + V2_THREADS / 64; kbk < nwhole; kbk += V2_THREADS / 64) {
     X6Row<KCH> kr, vr;
     x6_row_load<KCH>(kr, kb, p.k_st, (int64_t)kbk * 16 + li, p.Lk, lane, p.D);
     x6_row_load<KCH>(vr, vb, p.v_st, (int64_t)kbk * 16 + li, p.Lk, lane, p.D);
-    kblock(kbk, kr, vr);
+    f32x4 dkv[2 * DT];
+#pragma unroll
+    for (int i = 0; i < 2 * DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kblock(kbk, kr, vr, 0, nch, dkv);
+    kstore(kbk, dkv);
+  }
+  if (split) {
+    const int sb = nkb - 1, hc = nch / 2;
+    const bool own = wave == R - 1, part = wave == R;
+    f32x4 dkv[2 * DT];
+#pragma unroll
+    for (int i = 0; i < 2 * DT; ++i) dkv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (own || part) {
+      X6Row<KCH> kr, vr;
+      x6_row_load<KCH>(kr, kb, p.k_st, (int64_t)sb * 16 + li, p.Lk, lane, p.D);
+      x6_row_load<KCH>(vr, vb, p.v_st, (int64_t)sb * 16 + li, p.Lk, lane, p.D);
+      kblock(sb, kr, vr, own ? 0 : hc, own ? hc : nch, dkv);
+    }
+    __syncthreads();  // every wave is done with the Q / dO images: reuse them for the exchange
+    f32x4* xch = reinterpret_cast<f32x4*>(smem);
+    if (part) {
+#pragma unroll
+      for (int i = 0; i < 2 * DT; ++i) xch[i * 64 + lane] = dkv[i];
+    }
+    __syncthreads();
+    if (own) {
+#pragma unroll
+      for (int i = 0; i < 2 * DT; ++i) dkv[i] += xch[i * 64 + lane];
+      kstore(sb, dkv);
+    }
   }
 }
 
@@ -1621,7 +1724,8 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
   const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
-  auto qblock = [&](int qbk, const X6Row<KCH>& qr, const X6Row<KCH>& dr) {  // as kblock in dK/dV
+  // dQ of one query block over the key chunks [ka, kb2e) into dq (as kblock in dK/dV)
+  auto qblock = [&](int qbk, const X6Row<KCH>& qr, const X6Row<KCH>& dr, int ka, int kb2e, f32x4 (&dq)[DT]) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[3][KCH], dof[3][KCH];
     x6_row_split<KCH>(qf, qr);
@@ -1630,9 +1734,6 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
     const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
-    f32x4 dq[DT];
-#pragma unroll
-    for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto chunk = [&](int kc2, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-key subtiles of this 32-key chunk
       f32x4 sd[4];  // S^T (even) and dP^T (odd) per subtile
@@ -1698,8 +1799,12 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
       }
     };
     const int nfull = lk16 / 32;
-    for (int kc2 = 0; kc2 < nfull; ++kc2) chunk(kc2, std::integral_constant<int, 2>{});
-    if (lk16 & 16) chunk(nfull, std::integral_constant<int, 1>{});
+    const int ke = kb2e < nfull ? kb2e : nfull;
+    for (int kc2 = ka; kc2 < ke; ++kc2) chunk(kc2, std::integral_constant<int, 2>{});
+    if (kb2e > nfull) chunk(nfull, std::integral_constant<int, 1>{});
+  };
+  auto qstore = [&](int qbk, const f32x4 (&dq)[DT]) {
+    const int64_t q0 = (int64_t)qbk * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t q = q0 + 4 * g + r;
@@ -1720,12 +1825,52 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
     }
   };
   if (p.dbg & 2) return;
-  if (wave < nqb) qblock(wave, qn, don);
-  for (int qbk = wave + V2_THREADS / 64; qbk < nqb; qbk += V2_THREADS / 64) {
+  // the last query block halved over the key chunks between two SIMD pairs, as in dK/dV
+  const int nch = lk16 / 32 + ((lk16 & 16) ? 1 : 0);
+  const int R = nqb - V2_THREADS / 64;
+  const bool split = R >= 1 && R <= V2_THREADS / 64 && (R & 3) == 1 && nch >= 2;
+  const int nwhole = split ? nqb - 1 : nqb;
+  if (wave < nwhole) {
+    f32x4 dq[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    qblock(wave, qn, don, 0, nch, dq);
+    qstore(wave, dq);
+  }
+  for (int qbk = wave + V2_THREADS / 64; qbk < nwhole; qbk += V2_THREADS / 64) {
     X6Row<KCH> qr, dr;
     x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
     x6_row_load<KCH>(dr, dob, p.do_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
-    qblock(qbk, qr, dr);
+    f32x4 dq[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    qblock(qbk, qr, dr, 0, nch, dq);
+    qstore(qbk, dq);
+  }
+  if (split) {
+    const int sb = nqb - 1, hc = nch / 2;
+    const bool own = wave == R - 1, part = wave == R;
+    f32x4 dq[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (own || part) {
+      X6Row<KCH> qr, dr;
+      x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
+      x6_row_load<KCH>(dr, dob, p.do_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
+      qblock(sb, qr, dr, own ? 0 : hc, own ? hc : nch, dq);
+    }
+    __syncthreads();  // every wave is done with the K / V images: reuse them for the exchange
+    f32x4* xch = reinterpret_cast<f32x4*>(smem);
+    if (part) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) xch[d * 64 + lane] = dq[d];
+    }
+    __syncthreads();
+    if (own) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) dq[d] += xch[d * 64 + lane];
+      qstore(sb, dq);
+    }
   }
 }
 

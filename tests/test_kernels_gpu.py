@@ -267,7 +267,7 @@ def test_attention_fwd_bwd(dtype, case, masked, p):
 
 @pytest.mark.parametrize("case", [(4, 12, 128, 128, 64, True, 0.1), (3, 12, 197, 197, 64, False, 0.0),
                                   (2, 8, 128, 197, 32, True, 0.1), (2, 3, 208, 200, 48, True, 0.0),
-                                  (2, 2, 17, 45, 64, False, 0.1)])
+                                  (2, 2, 17, 45, 64, False, 0.1), (2, 4, 140, 140, 64, True, 0.1)])
 def test_attention_fp32_split_operands_error_matches_fp32_mfma(case):
     """fp32 attention on split bf16 operands (include/mmfd.h mmfd_set_fp32_attn_mode: every product
     from the hi/mid/lo planes, six MFMA products accumulated in fp32) against a float64 reference:
