@@ -1711,9 +1711,11 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   float* kbias = reinterpret_cast<float*>(smem + 6 * img);
   const float* qb = reinterpret_cast<const float*>(p.q) + b * p.q_sb + h * p.D;
   const float* dob = reinterpret_cast<const float*>(p.dout) + b * p.do_sb + h * p.D;
-  X6Row<KCH> qn, don;  // the wave's first query block, raw (loaded with the staging)
+  const float* obp = reinterpret_cast<const float*>(p.o) + b * p.o_sb + h * p.D;
+  X6Row<KCH> qn, don, on;  // the wave's first query block, raw (loaded with the staging)
   x6_row_load<KCH>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
   x6_row_load<KCH>(don, dob, p.do_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+  x6_row_load<KCH>(on, obp, p.o_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
   x6_stage2<D, V2_THREADS>(k_img, reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D, p.k_st, v_img,
                            reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D, p.v_st, img, p.Lk, lk16, tid,
                            p.D, p.dbg);
@@ -1725,13 +1727,27 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
   // dQ of one query block over the key chunks [ka, kb2e) into dq (as kblock in dK/dV)
-  auto qblock = [&](int qbk, const X6Row<KCH>& qr, const X6Row<KCH>& dr, int ka, int kb2e, f32x4 (&dq)[DT]) {
+  // delta = rowsum(dO * O) of the block's queries is computed here from the rows the wave loads
+  // anyway (no separate delta pass: the dQ kernel runs first and writes it for dK/dV)
+  auto qblock = [&](int qbk, const X6Row<KCH>& qr, const X6Row<KCH>& dr, const X6Row<KCH>& orow, bool wdelta,
+                    int ka, int kb2e, f32x4 (&dq)[DT]) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[3][KCH], dof[3][KCH];
     x6_row_split<KCH>(qf, qr);
     x6_row_split<KCH>(dof, dr);
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
-    const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+    float dsum = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < KCH; ++kc)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const float4 a = orow.v[kc][hh], c = dr.v[kc][hh];
+        dsum = fmaf(a.x, c.x, fmaf(a.y, c.y, fmaf(a.z, c.z, fmaf(a.w, c.w, dsum))));
+      }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    const float dlt = myq < p.Lq ? dsum : 0.f;
+    if (wdelta && g == 0 && myq < p.Lq) p.delta[bh * p.Lq + myq] = dsum;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
     auto chunk = [&](int kc2, auto nsc) {
@@ -1834,17 +1850,18 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
     f32x4 dq[DT];
 #pragma unroll
     for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    qblock(wave, qn, don, 0, nch, dq);
+    qblock(wave, qn, don, on, true, 0, nch, dq);
     qstore(wave, dq);
   }
   for (int qbk = wave + V2_THREADS / 64; qbk < nwhole; qbk += V2_THREADS / 64) {
-    X6Row<KCH> qr, dr;
+    X6Row<KCH> qr, dr, orr;
     x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
     x6_row_load<KCH>(dr, dob, p.do_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
+    x6_row_load<KCH>(orr, obp, p.o_st, (int64_t)qbk * 16 + li, p.Lq, lane, p.D);
     f32x4 dq[DT];
 #pragma unroll
     for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    qblock(qbk, qr, dr, 0, nch, dq);
+    qblock(qbk, qr, dr, orr, true, 0, nch, dq);
     qstore(qbk, dq);
   }
   if (split) {
@@ -1854,10 +1871,11 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
 #pragma unroll
     for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (own || part) {
-      X6Row<KCH> qr, dr;
+      X6Row<KCH> qr, dr, orr;
       x6_row_load<KCH>(qr, qb, p.q_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
       x6_row_load<KCH>(dr, dob, p.do_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
-      qblock(sb, qr, dr, own ? 0 : hc, own ? hc : nch, dq);
+      x6_row_load<KCH>(orr, obp, p.o_st, (int64_t)sb * 16 + li, p.Lq, lane, p.D);
+      qblock(sb, qr, dr, orr, own, own ? 0 : hc, own ? hc : nch, dq);
     }
     __syncthreads();  // every wave is done with the K / V images: reuse them for the exchange
     f32x4* xch = reinterpret_cast<f32x4*>(smem);
@@ -1899,14 +1917,12 @@ void launch_bwd_x6_d(const AttnP& p, hipStream_t s) {
   static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_x6_kernel<D, DROP>), X6A_LDS),
                       set_lds_attr(reinterpret_cast<const void*>(&attn_dq_x6_kernel<D, DROP>), X6A_LDS), true);
   (void)once;
-  const int64_t rows = p.B * p.H * p.Lq;
-  hipLaunchKernelGGL((attn_delta_kernel<float, D>), dim3((unsigned)((rows * AT<float, D>::NCH + 255) / 256)),
-                     dim3(256), 0, s, p);
+  // dQ first: it computes delta = rowsum(dO * O) for dK/dV (no separate delta pass)
   const int lq16 = v2_pad(p.Lq, 16), lk16 = v2_pad(p.Lk, 16);
-  hipLaunchKernelGGL((attn_dkdv_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
-                     6 * lq16 * X6A_RB + (2 * lq16 + lk16) * 4, s, p);
   hipLaunchKernelGGL((attn_dq_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
                      6 * lk16 * X6A_RB + lk16 * 4, s, p);
+  hipLaunchKernelGGL((attn_dkdv_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+                     6 * lq16 * X6A_RB + (2 * lq16 + lk16) * 4, s, p);
 }
 
 // dropout as a template argument: a run-time flag let the compiler if-convert the hash into every
