@@ -156,6 +156,22 @@ __device__ __forceinline__ uint4 pack_acc(const f32x4* s, int c) {
   }
 }
 
+// dot product of two 16-B chunks of T elements (fp32 sum)
+template <typename T>
+__device__ __forceinline__ float row_chunk_dot(const uint4& a, const uint4& b) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, a), y = __builtin_bit_cast(bf16x8, b);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = fmaf((float)x[e], (float)y[e], s);
+    return s;
+  } else {
+    return fmaf(__uint_as_float(a.x), __uint_as_float(b.x),
+                fmaf(__uint_as_float(a.y), __uint_as_float(b.y),
+                     fmaf(__uint_as_float(a.z), __uint_as_float(b.z), __uint_as_float(a.w) * __uint_as_float(b.w))));
+  }
+}
+
 // per-lane 16-B operand chunks of one row (query or key) held in registers
 template <typename T, int D>
 __device__ __forceinline__ void load_row_regs(uint4* f, const T* __restrict__ base, int64_t st,
@@ -979,7 +995,20 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
     load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
     load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
-    const float dlt = myq < p.Lq ? p.delta[bh * p.Lq + myq] : 0.f;
+    // delta = rowsum(dO * O) from the dO fragments in registers and the O row (this kernel runs
+    // before dK/dV and writes delta for it: no separate delta pass)
+    float dlt;
+    {
+      uint4 of[C::KCH];
+      load_row_regs<T, D>(of, reinterpret_cast<const T*>(p.o) + b * p.o_sb + h * p.D, p.o_st, myq, p.Lq, lane, p.D);
+      float ds = 0.f;
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) ds += row_chunk_dot<T>(of[kc], dof[kc]);
+      ds += __shfl_xor(ds, 16, 64);
+      ds += __shfl_xor(ds, 32, 64);
+      dlt = myq < p.Lq ? ds : 0.f;
+      if (g == 0 && myq < p.Lq) p.delta[bh * p.Lq + myq] = ds;
+    }
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     f32x4 dq[C::DT];
@@ -2016,9 +2045,7 @@ void launch_fwd_v2(const AttnP& p, hipStream_t s) {
 
 template <typename T, int D, bool REL>
 void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
-  const int64_t rows = p.B * p.H * p.Lq;
-  constexpr int nch = AT<T, D>::NCH, RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
-  hipLaunchKernelGGL((attn_delta_kernel<T, D>), dim3((unsigned)((rows * nch + 255) / 256)), dim3(256), 0, s, p);
+  constexpr int RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
   const int lq_pad = v2_pad(p.Lq, v2_kc<T>()), lk_pad = v2_pad(p.Lk, v2_kc<T>());
   constexpr int NI1 = V2<T, D>::DUAL ? 2 : 4, NI2 = V2<T, D>::DUAL ? 2 : 3;  // LDS images per kernel
   const int lds1 = NI1 * lq_pad * RB + 3 * V2_LMAX * 4;
@@ -2029,8 +2056,9 @@ void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
                                    NI2 * V2_LMAX * RB + V2_LMAX * 4),
                       true);
   (void)once;
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
+  // dQ first: it writes delta = rowsum(dO * O) for dK/dV (no separate delta pass)
   hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
 }
 
 template <typename T, int D>
