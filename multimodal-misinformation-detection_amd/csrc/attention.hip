@@ -46,6 +46,7 @@ struct AttnP {
   int acc_dq, acc_dkv;
   // fp32 backward: split planes of the packed [dq | dk | dv] buffer (base = dq), see mmfd_attn_args
   bf16* pl; int64_t pl_stride; const float* pl_base; int pl_only;
+  int idx32;  // every dropout index fits 32 bits (hash_c1)
   int dbg;  // x6 phase experiments (MMFD_X6A_DBG): 1 = stage zeros, 2 = skip the products
 };
 
@@ -59,6 +60,13 @@ __device__ __forceinline__ void plane_put(const AttnP& p, const float* dst, floa
   p.pl[off + p.pl_stride] = m;
   p.pl[off + 2 * p.pl_stride] = (bf16)(r - (float)m);
 }
+
+// Dropout with 32-bit indices (B*H*Lq*Lk <= 2^32: AttnP::idx32, required by the x6 kernels): mmfd_hash_k(key, idx) = mix32(key ^ lo(idx) * C1 ^
+// hi(idx) * C2) with hi(idx) = 0, and lo(idx) * C1 (mod 2^32) advances by additions — C1 per key,
+// Lk * C1 per query — so an element costs one v_add in place of the 64-bit index arithmetic and
+// its two extra 32-bit multiplies (bit-identical masks).
+constexpr uint32_t HASH_C1 = 0x9e3779b1u;
+__device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
 
 template <typename T, int D>
 struct AT {
@@ -673,6 +681,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
       if (cosine) cos_norm_q<D>(qf, qmult);
     }
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[C::DT];
@@ -753,12 +762,21 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(s[ks][r] - mnew);
           rs += e;
-          float pe = e;
-          if (p.p > 0.f) {
-            const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)(k0 + ks * 16 + 4 * g + r));
-            pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
+          s[ks][r] = e;
+        }
+        if (p.p > 0.f) {  // one uniform branch per subtile
+          if (p.idx32) {
+            const uint32_t c = rowc1 + (uint32_t)(k0 + ks * 16) * HASH_C1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              s[ks][r] = (hash_c1(hkey, c + (uint32_t)r * HASH_C1) < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)(k0 + ks * 16 + 4 * g + r));
+              s[ks][r] = (hsh < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
+            }
           }
-          s[ks][r] = pe;
         }
       }
       lsum = lsum * alpha + rs;  // per-lane partial over this lane's keys; reduced at the end
@@ -911,10 +929,17 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
         const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
         if (p.p > 0.f) {  // one uniform branch per subtile; the element index advances by Lk per query
-          uint64_t idx = hcol + (uint64_t)(qs * 16 + 4 * g) * (uint64_t)p.Lk;
+          if (p.idx32) {
+            const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
+            const uint32_t c = ((uint32_t)hcol + (uint32_t)(qs * 16 + 4 * g) * (uint32_t)p.Lk) * HASH_C1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r, idx += (uint64_t)p.Lk)
-            z[r] = (mmfd_hash_k(hkey, idx) < p.thr) ? 0.f : p.keep_scale;
+            for (int r = 0; r < 4; ++r) z[r] = (hash_c1(hkey, c + (uint32_t)r * lkc1) < p.thr) ? 0.f : p.keep_scale;
+          } else {
+            uint64_t idx = hcol + (uint64_t)(qs * 16 + 4 * g) * (uint64_t)p.Lk;
+#pragma unroll
+            for (int r = 0; r < 4; ++r, idx += (uint64_t)p.Lk)
+              z[r] = (mmfd_hash_k(hkey, idx) < p.thr) ? 0.f : p.keep_scale;
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1069,9 +1094,16 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
         const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
         if (p.p > 0.f) {  // one uniform branch per subtile
+          if (p.idx32) {
+            const uint32_t c = ((uint32_t)hrow + (uint32_t)(ks * 16 + 4 * g)) * HASH_C1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            z[r] = (mmfd_hash_k(hkey, hrow + (uint64_t)(ks * 16 + 4 * g + r)) < p.thr) ? 0.f : p.keep_scale;
+            for (int r = 0; r < 4; ++r)
+              z[r] = (hash_c1(hkey, c + (uint32_t)r * HASH_C1) < p.thr) ? 0.f : p.keep_scale;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              z[r] = (mmfd_hash_k(hkey, hrow + (uint64_t)(ks * 16 + 4 * g + r)) < p.thr) ? 0.f : p.keep_scale;
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1194,13 +1226,6 @@ __device__ __forceinline__ void split_acc(const f32x4& a, const f32x4& b, uint4&
   const float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   split8(x, hi, mid, lo);
 }
-
-// Dropout with 32-bit indices (B*H*Lq*Lk <= 2^32, x6_attn_ok): mmfd_hash_k(key, idx) = mix32(key ^ lo(idx) * C1 ^
-// hi(idx) * C2) with hi(idx) = 0, and lo(idx) * C1 (mod 2^32) advances by additions — C1 per key,
-// Lk * C1 per query — so an element costs one v_add in place of the 64-bit index arithmetic and
-// its two extra 32-bit multiplies (bit-identical masks).
-constexpr uint32_t HASH_C1 = 0x9e3779b1u;
-__device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
 
 // one fp32 row's MFMA fragments (lane: elements (kc*4 + g)*8 .. +7): loaded raw, split into planes
 // f[plane][kc] later (the loads of the next block issue before the current block's products)
@@ -2003,6 +2028,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.dv = a.dv; p.dv_sb = a.dv_sb; p.dv_st = a.dv_st;
   p.delta = a.delta;
   p.acc_dq = a.accumulate_dq; p.acc_dkv = a.accumulate_dkv;
+  p.idx32 = (uint64_t)a.B * (uint64_t)a.H * (uint64_t)a.Lq * (uint64_t)a.Lk <= (1ull << 32);
   static const int dbg = getenv("MMFD_X6A_DBG") ? atoi(getenv("MMFD_X6A_DBG")) : 0;
   p.dbg = dbg;
   return 0;
