@@ -21,8 +21,10 @@ if not os.path.exists(LIB):
     for f in sorted(os.listdir(SRC)):
         if f.endswith(".hip"):
             o = os.path.join(os.path.dirname(LIB), f + ".o")
-            subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950",
-                            "-DMMFD_G8_STAMPS", "-c", os.path.join(SRC, f), "-o", o], check=True)
+            extra = ["-fno-slp-vectorize"] if f == "gemm_x6f.hip" else []  # the product build's flags
+            subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950", "-mllvm",
+                            "-amdgpu-mfma-vgpr-form", *extra, "-DMMFD_G8_STAMPS", "-c", os.path.join(SRC, f), "-o", o],
+                           check=True)
             objs.append(o)
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", LIB] + objs, check=True)
 
