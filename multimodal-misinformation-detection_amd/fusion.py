@@ -14,6 +14,8 @@ residual add in its GEMM epilogue; dropout masks are generated in the epilogues.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import blocks as Bk
@@ -111,72 +113,194 @@ PATHS = [  # (claim modality, evidence modality, path tag, out proj, ln prefix)
     ("image", "text", "it", "image_text"),
     ("image", "image", "ii", "image_image"),
 ]
+PATH_OF = {(p[0], p[1]): p for p in PATHS}
+OTHER = {"text": "image", "image": "text"}
+
+_HEAD_SIDE = {}
+
+
+def _two_streams(*xs):
+    """whether the head's claim-text and claim-image halves run on two HIP streams: both
+    modalities present (the full four-path head) on a GPU, unless MMFD_SERIAL_HEAD=1"""
+    return (all(x is not None for x in xs) and xs[0].is_cuda and os.environ.get("MMFD_SERIAL_HEAD") != "1")
+
+
+def _head_stream(device):
+    s = _HEAD_SIDE.get(device.index)
+    if s is None:
+        s = _HEAD_SIDE[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+def _event():
+    e = torch.cuda.Event()
+    e.record()
+    return e
+
+
+def _kv_fwd(ctx, cfg, Em, m):
+    """evidence K|V of modality m: one GEMM (N = 2E) shared by both paths that read it"""
+    c = "cross_attn."
+    B, L, _ = Em.shape
+    return Bk.linear_packed(ctx, Bk.as2d(Em), [c + f"{m}_evidence_key", c + f"{m}_evidence_value"]).view(B, L, 2 * cfg.E)
+
+
+def _q_fwd(ctx, cfg, H, m):
+    """the claim modality's conditioning Q projection, shared by its two paths"""
+    B, L, _ = H.shape
+    return Bk.linear(ctx, Bk.as2d(H), f"cross_attn.{m}_WQ")[0].view(B, L, cfg.E)
+
+
+def _path_fwd(ctx, cfg, path, q, kv, H):
+    """one conditioning path (model.py:186-195 and its three siblings): LN(H + out(MHA(Q, K, V))),
+    then the claim modality's MLP block with the path's ln2"""
+    hm, em, tag, name = path
+    c = "cross_attn."
+    E = cfg.E
+    a, s1 = _attn_ln_fwd(ctx, cfg, q, kv[..., :E], kv[..., E:], Bk.as2d(H), c + f"{name}_out", c + f"{name}_ln1",
+                         c + tag)
+    S, s2 = Bk.mlp_ln_fwd(ctx, a, c + f"{hm}_mlp", c + f"{name}_ln2", c + tag + ".mlp", cfg.eps)
+    return S.view(H.shape), (s1, s2)
 
 
 def _cond_fwd(ctx, cfg, Hs, Es):
-    c = "cross_attn."
-    E = cfg.E
     Q, KV, out, st = {}, {}, {}, {}
     for m in ("text", "image"):
         if Hs.get(m) is not None and any(Es.get(e) is not None for e in ("text", "image")):
-            B, L, _ = Hs[m].shape
-            Q[m] = Bk.linear(ctx, Bk.as2d(Hs[m]), c + f"{m}_WQ")[0].view(B, L, E)
+            Q[m] = _q_fwd(ctx, cfg, Hs[m], m)
         if Es.get(m) is not None and any(Hs.get(x) is not None for x in ("text", "image")):
-            B, L, _ = Es[m].shape
-            KV[m] = Bk.linear_packed(ctx, Bk.as2d(Es[m]), [c + f"{m}_evidence_key", c + f"{m}_evidence_value"]
-                                     ).view(B, L, 2 * E)
-    for hm, em, tag, name in PATHS:
+            KV[m] = _kv_fwd(ctx, cfg, Es[m], m)
+    for path in PATHS:
+        hm, em, tag, _ = path
         if Hs.get(hm) is None or Es.get(em) is None:
             continue
-        kv = KV[em]
-        a, s1 = _attn_ln_fwd(ctx, cfg, Q[hm], kv[..., :E], kv[..., E:], Bk.as2d(Hs[hm]), c + f"{name}_out",
-                             c + f"{name}_ln1", c + tag)
-        S, s2 = Bk.mlp_ln_fwd(ctx, a, c + f"{hm}_mlp", c + f"{name}_ln2", c + tag + ".mlp", cfg.eps)
-        out[tag] = S.view(Hs[hm].shape)
-        st[tag] = (s1, s2)
+        out[tag], st[tag] = _path_fwd(ctx, cfg, path, Q[hm], KV[em], Hs[hm])
     return out, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
+
+
+def _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV):
+    """backward of one conditioning path: the residual gradient is summed into dH[claim modality],
+    the attention's dq into dQ[claim modality] and its dk|dv into dKV[evidence modality] (each
+    written by the first path that reaches it, accumulated by the second)"""
+    hm, em, tag, _ = path
+    E = cfg.E
+    s1, s2 = cst["st"][tag]
+    da = Bk.mlp_ln_bwd(ctx, Bk.as2d(dS[tag]), s2)
+    q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = s1
+    ds, _ = Bk.layernorm_bwd(ctx, da, s, ln_name, mean, rstd)
+    ctx.lin_grads([out_name], ds, Bk.as2d(o))
+    do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
+    # residual gradient into H, summed over the claim modality's two paths
+    if hm in dH:
+        K.axpby(1.0, dH[hm], 1.0, ds, out=dH[hm])
+    else:
+        dH[hm] = ds
+    first_q = hm not in dQ
+    first_kv = em not in dKV
+    if first_q:
+        dQ[hm] = torch.empty_like(q)
+    if first_kv:
+        dKV[em] = torch.empty_like(cst["KV"][em])
+    K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dQ[hm], dk=dKV[em][..., :E], dv=dKV[em][..., E:],
+               accumulate_dq=not first_q, accumulate_dkv=not first_kv, **ctx.drop(site + ".attn"))
+
+
+def _q_bwd(ctx, cfg, hm, dq, cst, dH):
+    """WQ gradients and dH[hm] += dQ WQ"""
+    dq2 = Bk.as2d(dq)
+    name = f"cross_attn.{hm}_WQ"
+    ctx.lin_grads([name], dq2, Bk.as2d(cst["Hs"][hm]))
+    Bk.linear_dx(ctx, dq2, name, out=dH[hm], beta=1.0)
+
+
+def _kv_bwd(ctx, cfg, em, dkv, cst, need, out=None):
+    """evidence K|V weight gradients; returns dE (or None when not needed)"""
+    names = [f"cross_attn.{em}_evidence_key", f"cross_attn.{em}_evidence_value"]
+    dkv2 = Bk.as2d(dkv)
+    ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]))
+    if not need:
+        return None
+    Wp, _ = ctx.w_packed(names)
+    return Bk.linear_dx(ctx, dkv2, Wp, out=out).view(cst["Es"][em].shape)
 
 
 def _cond_bwd(ctx, cfg, dS, cst, need_dE, out_dE=None):
     """dS: tag -> [B, L, E] grads. Returns (dH per claim modality (2-D), dE per evidence modality)."""
-    c = "cross_attn."
-    E = cfg.E
     dH, dQ, dKV = {}, {}, {}
-    for hm, em, tag, name in PATHS:
-        if tag not in cst["st"]:
-            continue
-        s1, s2 = cst["st"][tag]
-        da = Bk.mlp_ln_bwd(ctx, Bk.as2d(dS[tag]), s2)
-        q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = s1
-        ds, _ = Bk.layernorm_bwd(ctx, da, s, ln_name, mean, rstd)
-        ctx.lin_grads([out_name], ds, Bk.as2d(o))
-        do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
-        # residual gradient into H, summed over the claim modality's two paths
-        if hm in dH:
-            K.axpby(1.0, dH[hm], 1.0, ds, out=dH[hm])
-        else:
-            dH[hm] = ds
-        first_q = hm not in dQ
-        first_kv = em not in dKV
-        if first_q:
-            dQ[hm] = torch.empty_like(q)
-        if first_kv:
-            dKV[em] = torch.empty_like(cst["KV"][em])
-        K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dQ[hm], dk=dKV[em][..., :E], dv=dKV[em][..., E:],
-                   accumulate_dq=not first_q, accumulate_dkv=not first_kv, **ctx.drop(site + ".attn"))
+    for path in PATHS:
+        if path[2] in cst["st"]:
+            _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV)
     for hm, dq in dQ.items():
-        dq2 = Bk.as2d(dq)
-        ctx.lin_grads([c + f"{hm}_WQ"], dq2, Bk.as2d(cst["Hs"][hm]))
-        Bk.linear_dx(ctx, dq2, c + f"{hm}_WQ", out=dH[hm], beta=1.0)
+        _q_bwd(ctx, cfg, hm, dq, cst, dH)
     dE = {}
     for em, dkv in dKV.items():
-        names = [c + f"{em}_evidence_key", c + f"{em}_evidence_value"]
-        dkv2 = Bk.as2d(dkv)
-        ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]))
-        if need_dE.get(em):
-            Wp, _ = ctx.w_packed(names)
-            dE[em] = Bk.linear_dx(ctx, dkv2, Wp, out=(out_dE or {}).get(em)).view(cst["Es"][em].shape)
+        d = _kv_bwd(ctx, cfg, em, dkv, cst, need_dE.get(em), (out_dE or {}).get(em))
+        if d is not None:
+            dE[em] = d
     return dH, dE
+
+
+def _fwd_two_streams(ctx, cfg, Xs, Es):
+    """Representation + conditioning with the claim-text half (representation, Q, paths tt and ti)
+    on the current stream and the claim-image half (it, ii) on a second one. The head's GEMMs have
+    N = E = 256 and K = 256-1024: one 256x256 tile column over B*L rows leaves half the CUs idle
+    (128 tiles for text, 197 for image), and the two halves only meet at the evidence K|V, which
+    each stream computes first and publishes by an event. Same kernels and values as _cond_fwd."""
+    main = torch.cuda.current_stream()
+    side = _head_stream(Xs["text"].device)
+    side.wait_stream(main)
+    streams = {"text": main, "image": side}
+    Hs, rst, Q, KV, ev, out, st = {}, {}, {}, {}, {}, {}, {}
+    for m in ("text", "image"):
+        with torch.cuda.stream(streams[m]):
+            KV[m] = _kv_fwd(ctx, cfg, Es[m], m)
+            ev[m] = _event()
+    for m in ("text", "image"):
+        with torch.cuda.stream(streams[m]):
+            Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, Xs[m], m, unimodal=False)
+            Q[m] = _q_fwd(ctx, cfg, Hs[m], m)
+            for em in (m, OTHER[m]):  # own evidence first: the other stream's K|V may still be running
+                if em != m:
+                    torch.cuda.current_stream().wait_event(ev[em])
+                path = PATH_OF[(m, em)]
+                out[path[2]], st[path[2]] = _path_fwd(ctx, cfg, path, Q[m], KV[em], Hs[m])
+    main.wait_stream(side)
+    # (every tensor one stream reads from the other stays referenced by the head state until the
+    # backward has joined both streams again, so the caching allocator cannot hand its memory to
+    # the producing stream while the reader may still be queued)
+    return Hs, rst, {t: out[t] for t in ("tt", "ti", "it", "ii")}, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
+
+
+def _bwd_two_streams(ctx, cfg, dS, state, need_dX, need_e, outs):
+    """head_backward's conditioning + representation part on the streams of _fwd_two_streams. Each
+    stream accumulates its own paths' dk|dv per evidence modality; after both have published theirs
+    (events), the evidence modality's stream sums the two (fp32: the same value as the serial
+    in-kernel accumulation) and runs the evidence K|V gradients."""
+    cst = state["cst"]
+    main = torch.cuda.current_stream()
+    side = _head_stream(dS["tt"].device)
+    side.wait_stream(main)
+    streams = {"text": main, "image": side}
+    dKVs, ev, dX, dE = {}, {}, {}, {}
+    for m in ("text", "image"):
+        with torch.cuda.stream(streams[m]):
+            dH, dQ, dKV = {}, {}, {}
+            for path in PATHS:
+                if path[0] == m:
+                    _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV)
+            dKVs[m] = dKV
+            ev[m] = _event()
+            _q_bwd(ctx, cfg, m, dQ[m], cst, dH)
+            dX[m] = _repr_modality_bwd(ctx, cfg, dH[m], state["rst"][m], need_dX[m], out=outs[m])
+    for em in ("text", "image"):
+        with torch.cuda.stream(streams[em]):
+            torch.cuda.current_stream().wait_event(ev[OTHER[em]])
+            # claim-text path first, as the serial PATHS order accumulates
+            dkv = dKVs[em][em]
+            K.axpby(1.0, dKVs["text"][em], 1.0, dKVs["image"][em], out=dkv)
+            dE[em] = _kv_bwd(ctx, cfg, em, dkv, cst, need_e[em], outs["E" + em])
+    main.wait_stream(side)
+    return dX, dE
 
 
 # -------------------------------------------------------------------------------------------------
@@ -225,10 +349,15 @@ def head_forward(ctx, cfg: HeadConfig, X_t, X_i, E_t, E_i):
         X_i = E_i = None
     Hs, rst = {}, {}
     uni = (X_t is None) != (X_i is None) or cfg.text_only
-    for m, x in (("text", X_t), ("image", X_i)):
-        if x is not None:
-            Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, x, m, unimodal=uni)
-    S, cst = _cond_fwd(ctx, cfg, Hs, {"text": E_t, "image": E_i})
+    Es = {"text": E_t, "image": E_i}
+    two = not uni and _two_streams(X_t, X_i, E_t, E_i)
+    if two:
+        Hs, rst, S, cst = _fwd_two_streams(ctx, cfg, {"text": X_t, "image": X_i}, Es)
+    else:
+        for m, x in (("text", X_t), ("image", X_i)):
+            if x is not None:
+                Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, x, m, unimodal=uni)
+        S, cst = _cond_fwd(ctx, cfg, Hs, Es)
     pooled, hst, outs = {}, {}, {}
     if cfg.text_only:
         p = K.seq_mean_fwd(S["tt"])
@@ -248,7 +377,7 @@ def head_forward(ctx, cfg: HeadConfig, X_t, X_i, E_t, E_i):
                 p = K.seq_mean_fwd(S[t])
                 name = "classifier." + CLS_NAMES[t]
                 outs[t], hst[t] = _mlp_head_fwd(ctx, p, name, 1, name)
-    state = dict(rst=rst, cst=cst, S=S, hst=hst, shapes={m: x.shape for m, x in (("text", X_t), ("image", X_i))
+    state = dict(rst=rst, cst=cst, S=S, hst=hst, two=two, shapes={m: x.shape for m, x in (("text", X_t), ("image", X_i))
                                                           if x is not None})
     return outs, state
 
@@ -273,6 +402,10 @@ def head_backward(ctx, cfg: HeadConfig, douts, state, need_dX=(True, True), need
             dp = _mlp_head_bwd(ctx, douts[t], st)
             dS[t] = K.seq_mean_bwd(dp, S[t].shape[1])
     need_e = {"text": need_dE[0], "image": need_dE[1]}
+    if state.get("two"):
+        dX, dE = _bwd_two_streams(ctx, cfg, dS, state, {"text": need_dX[0], "image": need_dX[1]}, need_e,
+                                  {"text": outs[0], "image": outs[1], "Etext": outs[2], "Eimage": outs[3]})
+        return dX.get("text"), dX.get("image"), dE.get("text"), dE.get("image")
     dH, dE = _cond_bwd(ctx, cfg, dS, state["cst"], need_e, out_dE={"text": outs[2], "image": outs[3]})
     dX = {}
     for m, st in state["rst"].items():

@@ -195,3 +195,41 @@ def test_full_dims_factify_shapes_vs_oracle():
         (ar, br), (cr, dr) = OF.model_forward(P, *X, num_heads=8)
     for y, r in zip((a, b, c, d), (ar, br, cr, dr)):
         _close(y, r, 1e-4)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_two_stream_head_matches_serial(monkeypatch, precision):
+    """The head's claim-text / claim-image halves on two HIP streams (fusion._fwd_two_streams /
+    _bwd_two_streams) against MMFD_SERIAL_HEAD=1 at full head dims (E=256, 8 heads, text 128 and
+    image 197 rows, B=8), train mode with dropout 0.1: fp32 logits and every gradient bit-identical
+    (the evidence dk|dv sum is the same fp32 addition the serial in-kernel accumulation does); bf16:
+    the two-stream sum rounds the second path's dk|dv to bf16 once more, so the logits and the input
+    gradients agree to 5e-2 in relative norm (small parameter gradients are bf16 noise there)."""
+    g = torch.Generator().manual_seed(11)
+    X = [torch.randn(8, 128, 768, generator=g), torch.randn(8, 197, 768, generator=g),
+         torch.randn(8, 128, 768, generator=g), torch.randn(8, 197, 768, generator=g)]
+    m = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768, dropout=0.1).to(DEV).train()
+    if precision == "bf16":
+        m.set_precision("bf16")
+    R = [torch.randn(8, 3, generator=g).to(DEV) for _ in range(4)]
+
+    def run(serial):
+        monkeypatch.setenv("MMFD_SERIAL_HEAD", "1" if serial else "0")
+        m.manual_seed(77)
+        m.zero_grad(set_to_none=True)
+        Xg = [x.to(DEV).requires_grad_(True) for x in X]
+        (a, b), (c, d) = m(*Xg)
+        sum((y * r).sum() for y, r in zip((a, b, c, d), R)).backward()
+        torch.cuda.synchronize()
+        return ([y.detach().clone() for y in (a, b, c, d)], [x.grad.clone() for x in Xg],
+                {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+
+    ys, xs, ps = run(True)
+    yt, xt, pt = run(False)
+    assert ps.keys() == pt.keys()
+    if precision == "fp32":
+        for s, t in list(zip(ys, yt)) + list(zip(xs, xt)) + [(ps[n], pt[n]) for n in ps]:
+            assert torch.equal(s, t)
+    else:
+        for s, t in list(zip(ys, yt)) + list(zip(xs, xt)):
+            assert (s.float() - t.float()).norm().item() <= 5e-2 * s.float().norm().item()
