@@ -417,21 +417,35 @@ def layernorm_bwd(ctx: StepCtx, dy2d, x2d, name, mean, rstd, *, dx_add=None, dro
 # -------------------------------------------------------------------------------------------------
 # MLP block:  y = LN(a + drop(W2 drop(gelu(W1 a + b1)) + b2))     (layers.py:12-18 + model.py:109)
 # -------------------------------------------------------------------------------------------------
-def mlp_ln_fwd(ctx: StepCtx, a2d, mlp, ln, site, eps=1e-5, w1=".net.0", w2=".net.3"):
-    h, pre = linear(ctx, a2d, mlp + w1, act=K.ACT_GELU, keep_aux=True, drop_site=site + ".h")
-    s, _ = linear(ctx, h, mlp + w2, residual=a2d, drop_site=site + ".out")
-    y, mean, rstd = layernorm(ctx, s, ln, eps)
-    return y, (a2d, h, pre, s, mean, rstd, mlp, ln, site, w1, w2)
+def mlp_ln_fwd(ctx: StepCtx, a2d, mlp, ln, site, eps=1e-5, w1=".net.0", w2=".net.3", ap=None, want_planes=False):
+    """`ap`: split planes of a2d (split-operand fp32 mode, else None); the hidden activation's planes
+    come from the W1 epilogue (no fp32 copy when both of its GEMMs run on split operands), and with
+    `want_planes` the LayerNorm also writes the output's planes. Returns (y, yp or None, state)."""
+    T, E = a2d.shape
+    I = ctx.P[mlp + w1 + ".weight"].shape[0]
+    hp, h_out = out_planes(ctx, T, I, [(T, E, I), (E, I, T, True, True)], a2d.device) if ap is not None \
+        else (None, True)
+    h, pre = linear(ctx, a2d, mlp + w1, act=K.ACT_GELU, keep_aux=True, drop_site=site + ".h", xp=ap, out_planes=hp,
+                    write_out=h_out)
+    s, _ = linear(ctx, h, mlp + w2, residual=a2d, drop_site=site + ".out", xp=hp)
+    y, mean, rstd, yp = layernorm_planes(ctx, s, ln, eps, want=want_planes)
+    return y, yp, (a2d, ap, h, hp, pre, s, mean, rstd, mlp, ln, site, w1, w2)
 
 
 def mlp_ln_bwd(ctx: StepCtx, dy2d, st):
-    a2d, h, pre, s, mean, rstd, mlp, ln, site, w1, w2 = st
-    ds, ds_drop = layernorm_bwd(ctx, dy2d, s, ln, mean, rstd, drop_site=site + ".out")
+    a2d, ap, h, hp, pre, s, mean, rstd, mlp, ln, site, w1, w2 = st
+    ds, ds_drop, gp = layernorm_bwd_planes(ctx, dy2d, s, ln, mean, rstd, drop_site=site + ".out") \
+        if ap is not None else (*layernorm_bwd(ctx, dy2d, s, ln, mean, rstd, drop_site=site + ".out"), None)
     g_out = ds_drop if ds_drop is not None else ds
-    ctx.lin_grads([mlp + w2], g_out, h)
-    dpre = linear_dx(ctx, g_out, mlp + w2, act=K.ACT_GELU_BWD, aux=pre, drop_site=site + ".h")
-    ctx.lin_grads([mlp + w1], dpre, a2d)
-    linear_dx(ctx, dpre, mlp + w1, out=ds, beta=1.0)  # da = ds + dpre W1
+    ctx.lin_grads([mlp + w2], g_out, h, gp, hp)
+    T, E = g_out.shape
+    I = h.shape[1]
+    dprep, dpre_out = out_planes(ctx, T, I, [(I, E, T, True, True), (T, E, I, False, True)], g_out.device) \
+        if gp is not None else (None, True)
+    dpre = linear_dx(ctx, g_out, mlp + w2, act=K.ACT_GELU_BWD, aux=pre, drop_site=site + ".h", dyp=gp,
+                     out_planes=dprep, write_out=dpre_out)
+    ctx.lin_grads([mlp + w1], dpre, a2d, dprep, ap)
+    linear_dx(ctx, dpre, mlp + w1, out=ds, beta=1.0, dyp=dprep)  # da = ds + dpre W1
     return ds
 
 

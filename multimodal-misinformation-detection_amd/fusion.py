@@ -34,22 +34,39 @@ class HeadConfig:
 # -------------------------------------------------------------------------------------------------
 # attention block: y = LN(res + out_proj(MHA(q, k, v)))
 # -------------------------------------------------------------------------------------------------
-def _attn_ln_fwd(ctx, cfg, q, k, v, res2d, out_name, ln_name, site):
+# Split-operand fp32 mode (Bk.StepCtx.planes): every GEMM input of the head is split into its bf16
+# planes once, by its producer where one can (attention output, GEMM epilogue, LayerNorm forward /
+# backward), else by one split3 pass, and the planes are kept for the weight-gradient GEMM; every
+# output gradient is split once for its data- and weight-gradient GEMMs. All planes are None in
+# bf16 / fp32-MFMA mode.
+def _attn_ln_fwd(ctx, cfg, q, k, v, res2d, out_name, ln_name, site, want_planes=False):
+    """(y, y planes or None, state)"""
     B, Lq, _ = q.shape
-    o, lse = K.attn_fwd(q, k, v, cfg.H, **ctx.drop(site + ".attn"))
-    s, _ = Bk.linear(ctx, Bk.as2d(o), out_name, residual=res2d)
-    y, mean, rstd = Bk.layernorm(ctx, s, ln_name, cfg.eps)
-    return y, (q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site)
+    op = Bk.new_planes(ctx, B * Lq, q.shape[2], q.device)
+    o, lse = K.attn_fwd(q, k, v, cfg.H, o_planes=op, **ctx.drop(site + ".attn"))
+    s, _ = Bk.linear(ctx, Bk.as2d(o), out_name, residual=res2d, xp=op)
+    y, mean, rstd, yp = Bk.layernorm_planes(ctx, s, ln_name, cfg.eps, want=want_planes)
+    return y, yp, (q, k, v, o, op, lse, s, mean, rstd, out_name, ln_name, site)
 
 
-def _attn_ln_bwd(ctx, cfg, dy2d, st, *, dq=None, acc_dq=False, dk=None, dv=None, acc_dkv=False):
+def _attn_ln_out_bwd(ctx, dy2d, st):
+    """LayerNorm + output-projection backward of an attention block: (ds, do)"""
+    q, k, v, o, op, lse, s, mean, rstd, out_name, ln_name, site = st
+    if op is not None:
+        ds, _, dsp = Bk.layernorm_bwd_planes(ctx, dy2d, s, ln_name, mean, rstd)
+    else:
+        (ds, _), dsp = Bk.layernorm_bwd(ctx, dy2d, s, ln_name, mean, rstd), None
+    ctx.lin_grads([out_name], ds, Bk.as2d(o), dsp, op)
+    do = Bk.linear_dx(ctx, ds, out_name, dyp=dsp).view(o.shape)
+    return ds, do
+
+
+def _attn_ln_bwd(ctx, cfg, dy2d, st, *, dq=None, acc_dq=False, dk=None, dv=None, acc_dkv=False, dqkv_planes=None):
     """Returns ds (the gradient of the residual input); writes/accumulates dq, dk, dv."""
-    q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = st
-    ds, _ = Bk.layernorm_bwd(ctx, dy2d, s, ln_name, mean, rstd)
-    ctx.lin_grads([out_name], ds, Bk.as2d(o))
-    do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
+    q, k, v, o, op, lse, s, mean, rstd, out_name, ln_name, site = st
+    ds, do = _attn_ln_out_bwd(ctx, dy2d, st)
     K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dq, dk=dk, dv=dv, accumulate_dq=acc_dq, accumulate_dkv=acc_dkv,
-               **ctx.drop(site + ".attn"))
+               dqkv_planes=dqkv_planes, **ctx.drop(site + ".attn"))
     return ds
 
 
@@ -60,17 +77,27 @@ def _repr_modality_fwd(ctx, cfg, Xin, m, unimodal):
     r = "representation."
     B, L, _ = Xin.shape
     E = cfg.E
-    X, _ = Bk.linear(ctx, Bk.as2d(Xin), r + f"{m}_proj")
-    qkv = Bk.linear_packed(ctx, X, [r + f"{m}_WQ", r + f"{m}_WK", r + f"{m}_WV"]).view(B, L, 3 * E)
+    x2d = Bk.as2d(Xin)
+    xinp = ctx.planes(x2d)
+    # X feeds the QKV GEMM (planes from the projection's epilogue) and the self-attention residual
+    Xp = Bk.out_planes(ctx, B * L, E, (), Xin.device)[0] if xinp is not None else None
+    X, _ = Bk.linear(ctx, x2d, r + f"{m}_proj", xp=xinp, out_planes=Xp)
+    qkv = Bk.linear_packed(ctx, X, [r + f"{m}_WQ", r + f"{m}_WK", r + f"{m}_WV"], xp=Xp).view(B, L, 3 * E)
     q, k, v = qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]
-    Hh, st1 = _attn_ln_fwd(ctx, cfg, q, k, v, X, r + f"{m}_self_attn_out", r + f"{m}_self_ln1", r + f"{m}.self")
+    sp = xinp is not None
+    Hh, Hp, st1 = _attn_ln_fwd(ctx, cfg, q, k, v, X, r + f"{m}_self_attn_out", r + f"{m}_self_ln1", r + f"{m}.self",
+                               want_planes=unimodal and sp)
+    st = dict(Xin=Xin, xinp=xinp, X=X, Xp=Xp, qkv=qkv, st1=st1, st2=None, m=m)
     if unimodal:  # model.py:83-100: self-attention, then MLP + self_ln2
-        Y, st3 = Bk.mlp_ln_fwd(ctx, Hh, r + f"{m}_mlp", r + f"{m}_self_ln2", r + f"{m}.mlp", cfg.eps)
-        return Y.view(B, L, E), dict(Xin=Xin, X=X, qkv=qkv, st1=st1, st2=None, st3=st3, m=m)
+        Y, Yp, st["st3"] = Bk.mlp_ln_fwd(ctx, Hh, r + f"{m}_mlp", r + f"{m}_self_ln2", r + f"{m}.mlp", cfg.eps, ap=Hp,
+                                         want_planes=sp)
+        return Y.view(B, L, E), Yp, st
     Hv = Hh.view(B, L, E)
-    C, st2 = _attn_ln_fwd(ctx, cfg, Hv, k, v, Hh, r + f"{m}_cross_attn_out", r + f"{m}_cross_ln1", r + f"{m}.cross")
-    Y, st3 = Bk.mlp_ln_fwd(ctx, C, r + f"{m}_mlp", r + f"{m}_cross_ln2", r + f"{m}.mlp", cfg.eps)
-    return Y.view(B, L, E), dict(Xin=Xin, X=X, qkv=qkv, st1=st1, st2=st2, st3=st3, m=m)
+    C, Cp, st["st2"] = _attn_ln_fwd(ctx, cfg, Hv, k, v, Hh, r + f"{m}_cross_attn_out", r + f"{m}_cross_ln1",
+                                    r + f"{m}.cross", want_planes=sp)
+    Y, Yp, st["st3"] = Bk.mlp_ln_fwd(ctx, C, r + f"{m}_mlp", r + f"{m}_cross_ln2", r + f"{m}.mlp", cfg.eps, ap=Cp,
+                                     want_planes=sp)
+    return Y.view(B, L, E), Yp, st
 
 
 def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin, out=None):
@@ -80,28 +107,30 @@ def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin, out=None):
     qkv = st["qkv"]
     B, L, _ = qkv.shape
     dqkv = torch.empty_like(qkv)
+    # the packed dQ|dK|dV's planes come from the last attention backward that writes it
+    dqkvp = Bk.new_planes(ctx, B * L, 3 * E, qkv.device) if st["Xp"] is not None else None
     dC = Bk.mlp_ln_bwd(ctx, dY2d, st["st3"])
     if st["st2"] is not None:
-        q2, k2, v2, o2, lse2, s2, mean2, rstd2, out2, ln2, site2 = st["st2"]
-        ds2, _ = Bk.layernorm_bwd(ctx, dC, s2, ln2, mean2, rstd2)      # dH (residual part)
-        ctx.lin_grads([out2], ds2, Bk.as2d(o2))
-        do2 = Bk.linear_dx(ctx, ds2, out2).view(o2.shape)
+        q2, k2, v2, o2, _, lse2, _, _, _, _, _, site2 = st["st2"]
+        ds2, do2 = _attn_ln_out_bwd(ctx, dC, st["st2"])      # ds2: dH (residual part)
         # dq of the cross attention goes straight into dH (= ds2), dk/dv start dQKV's K|V blocks
         K.attn_bwd(q2, k2, v2, o2, lse2, do2, cfg.H, dq=ds2.view(B, L, E), dk=dqkv[..., E:2 * E],
                    dv=dqkv[..., 2 * E:], accumulate_dq=True, accumulate_dkv=False, **ctx.drop(site2 + ".attn"))
         dX = _attn_ln_bwd(ctx, cfg, ds2, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:],
-                          acc_dkv=True)
+                          acc_dkv=True, dqkv_planes=dqkvp)
     else:
-        dX = _attn_ln_bwd(ctx, cfg, dC, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:])
+        dX = _attn_ln_bwd(ctx, cfg, dC, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:],
+                          dqkv_planes=dqkvp)
     dqkv2 = Bk.as2d(dqkv)
     names = [r + f"{m}_WQ", r + f"{m}_WK", r + f"{m}_WV"]
-    ctx.lin_grads(names, dqkv2, st["X"])
+    ctx.lin_grads(names, dqkv2, st["X"], dqkvp, st["Xp"])
     Wp, _ = ctx.w_packed(names)
-    Bk.linear_dx(ctx, dqkv2, Wp, out=dX, beta=1.0)  # dX += dQKV [WQ;WK;WV]
-    ctx.lin_grads([r + f"{m}_proj"], dX, Bk.as2d(st["Xin"]))
+    Bk.linear_dx(ctx, dqkv2, Wp, out=dX, beta=1.0, dyp=dqkvp)  # dX += dQKV [WQ;WK;WV]
+    dXp = ctx.planes(dX) if st["xinp"] is not None else None
+    ctx.lin_grads([r + f"{m}_proj"], dX, Bk.as2d(st["Xin"]), dXp, st["xinp"])
     if not need_dxin:
         return None
-    return Bk.linear_dx(ctx, dX, r + f"{m}_proj", out=out).view(st["Xin"].shape)
+    return Bk.linear_dx(ctx, dX, r + f"{m}_proj", out=out, dyp=dXp).view(st["Xin"].shape)
 
 
 # -------------------------------------------------------------------------------------------------
@@ -138,17 +167,21 @@ def _event():
     return e
 
 
-def _kv_fwd(ctx, cfg, Em, m):
-    """evidence K|V of modality m: one GEMM (N = 2E) shared by both paths that read it"""
+def _kv_fwd(ctx, cfg, Em, m, EP):
+    """evidence K|V of modality m: one GEMM (N = 2E) shared by both paths that read it; the
+    evidence's planes go to EP[m] for the weight-gradient GEMM"""
     c = "cross_attn."
     B, L, _ = Em.shape
-    return Bk.linear_packed(ctx, Bk.as2d(Em), [c + f"{m}_evidence_key", c + f"{m}_evidence_value"]).view(B, L, 2 * cfg.E)
+    e2d = Bk.as2d(Em)
+    EP[m] = ctx.planes(e2d)
+    return Bk.linear_packed(ctx, e2d, [c + f"{m}_evidence_key", c + f"{m}_evidence_value"], xp=EP[m]
+                            ).view(B, L, 2 * cfg.E)
 
 
-def _q_fwd(ctx, cfg, H, m):
+def _q_fwd(ctx, cfg, H, Hp, m):
     """the claim modality's conditioning Q projection, shared by its two paths"""
     B, L, _ = H.shape
-    return Bk.linear(ctx, Bk.as2d(H), f"cross_attn.{m}_WQ")[0].view(B, L, cfg.E)
+    return Bk.linear(ctx, Bk.as2d(H), f"cross_attn.{m}_WQ", xp=Hp)[0].view(B, L, cfg.E)
 
 
 def _path_fwd(ctx, cfg, path, q, kv, H):
@@ -157,25 +190,25 @@ def _path_fwd(ctx, cfg, path, q, kv, H):
     hm, em, tag, name = path
     c = "cross_attn."
     E = cfg.E
-    a, s1 = _attn_ln_fwd(ctx, cfg, q, kv[..., :E], kv[..., E:], Bk.as2d(H), c + f"{name}_out", c + f"{name}_ln1",
-                         c + tag)
-    S, s2 = Bk.mlp_ln_fwd(ctx, a, c + f"{hm}_mlp", c + f"{name}_ln2", c + tag + ".mlp", cfg.eps)
+    a, ap, s1 = _attn_ln_fwd(ctx, cfg, q, kv[..., :E], kv[..., E:], Bk.as2d(H), c + f"{name}_out",
+                             c + f"{name}_ln1", c + tag, want_planes=True)
+    S, _, s2 = Bk.mlp_ln_fwd(ctx, a, c + f"{hm}_mlp", c + f"{name}_ln2", c + tag + ".mlp", cfg.eps, ap=ap)
     return S.view(H.shape), (s1, s2)
 
 
-def _cond_fwd(ctx, cfg, Hs, Es):
-    Q, KV, out, st = {}, {}, {}, {}
+def _cond_fwd(ctx, cfg, Hs, HP, Es):
+    Q, KV, EP, out, st = {}, {}, {}, {}, {}
     for m in ("text", "image"):
         if Hs.get(m) is not None and any(Es.get(e) is not None for e in ("text", "image")):
-            Q[m] = _q_fwd(ctx, cfg, Hs[m], m)
+            Q[m] = _q_fwd(ctx, cfg, Hs[m], HP.get(m), m)
         if Es.get(m) is not None and any(Hs.get(x) is not None for x in ("text", "image")):
-            KV[m] = _kv_fwd(ctx, cfg, Es[m], m)
+            KV[m] = _kv_fwd(ctx, cfg, Es[m], m, EP)
     for path in PATHS:
         hm, em, tag, _ = path
         if Hs.get(hm) is None or Es.get(em) is None:
             continue
         out[tag], st[tag] = _path_fwd(ctx, cfg, path, Q[hm], KV[em], Hs[hm])
-    return out, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
+    return out, dict(Q=Q, KV=KV, st=st, Hs=Hs, HP=HP, Es=Es, EP=EP)
 
 
 def _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV):
@@ -186,10 +219,8 @@ def _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV):
     E = cfg.E
     s1, s2 = cst["st"][tag]
     da = Bk.mlp_ln_bwd(ctx, Bk.as2d(dS[tag]), s2)
-    q, k, v, o, lse, s, mean, rstd, out_name, ln_name, site = s1
-    ds, _ = Bk.layernorm_bwd(ctx, da, s, ln_name, mean, rstd)
-    ctx.lin_grads([out_name], ds, Bk.as2d(o))
-    do = Bk.linear_dx(ctx, ds, out_name).view(o.shape)
+    q, k, v, o, _, lse, _, _, _, _, _, site = s1
+    ds, do = _attn_ln_out_bwd(ctx, da, s1)
     # residual gradient into H, summed over the claim modality's two paths
     if hm in dH:
         K.axpby(1.0, dH[hm], 1.0, ds, out=dH[hm])
@@ -209,19 +240,23 @@ def _q_bwd(ctx, cfg, hm, dq, cst, dH):
     """WQ gradients and dH[hm] += dQ WQ"""
     dq2 = Bk.as2d(dq)
     name = f"cross_attn.{hm}_WQ"
-    ctx.lin_grads([name], dq2, Bk.as2d(cst["Hs"][hm]))
-    Bk.linear_dx(ctx, dq2, name, out=dH[hm], beta=1.0)
+    hp = cst["HP"].get(hm)
+    dqp = ctx.planes(dq2) if hp is not None else None
+    ctx.lin_grads([name], dq2, Bk.as2d(cst["Hs"][hm]), dqp, hp)
+    Bk.linear_dx(ctx, dq2, name, out=dH[hm], beta=1.0, dyp=dqp)
 
 
 def _kv_bwd(ctx, cfg, em, dkv, cst, need, out=None):
     """evidence K|V weight gradients; returns dE (or None when not needed)"""
     names = [f"cross_attn.{em}_evidence_key", f"cross_attn.{em}_evidence_value"]
     dkv2 = Bk.as2d(dkv)
-    ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]))
+    ep = cst["EP"].get(em)
+    dkvp = ctx.planes(dkv2) if ep is not None else None
+    ctx.lin_grads(names, dkv2, Bk.as2d(cst["Es"][em]), dkvp, ep)
     if not need:
         return None
     Wp, _ = ctx.w_packed(names)
-    return Bk.linear_dx(ctx, dkv2, Wp, out=out).view(cst["Es"][em].shape)
+    return Bk.linear_dx(ctx, dkv2, Wp, out=out, dyp=dkvp).view(cst["Es"][em].shape)
 
 
 def _cond_bwd(ctx, cfg, dS, cst, need_dE, out_dE=None):
@@ -250,15 +285,15 @@ def _fwd_two_streams(ctx, cfg, Xs, Es):
     side = _head_stream(Xs["text"].device)
     side.wait_stream(main)
     streams = {"text": main, "image": side}
-    Hs, rst, Q, KV, ev, out, st = {}, {}, {}, {}, {}, {}, {}
+    Hs, HP, EP, rst, Q, KV, ev, out, st = {}, {}, {}, {}, {}, {}, {}, {}, {}
     for m in ("text", "image"):
         with torch.cuda.stream(streams[m]):
-            KV[m] = _kv_fwd(ctx, cfg, Es[m], m)
+            KV[m] = _kv_fwd(ctx, cfg, Es[m], m, EP)
             ev[m] = _event()
     for m in ("text", "image"):
         with torch.cuda.stream(streams[m]):
-            Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, Xs[m], m, unimodal=False)
-            Q[m] = _q_fwd(ctx, cfg, Hs[m], m)
+            Hs[m], HP[m], rst[m] = _repr_modality_fwd(ctx, cfg, Xs[m], m, unimodal=False)
+            Q[m] = _q_fwd(ctx, cfg, Hs[m], HP[m], m)
             for em in (m, OTHER[m]):  # own evidence first: the other stream's K|V may still be running
                 if em != m:
                     torch.cuda.current_stream().wait_event(ev[em])
@@ -268,7 +303,8 @@ def _fwd_two_streams(ctx, cfg, Xs, Es):
     # (every tensor one stream reads from the other stays referenced by the head state until the
     # backward has joined both streams again, so the caching allocator cannot hand its memory to
     # the producing stream while the reader may still be queued)
-    return Hs, rst, {t: out[t] for t in ("tt", "ti", "it", "ii")}, dict(Q=Q, KV=KV, st=st, Hs=Hs, Es=Es)
+    return Hs, rst, {t: out[t] for t in ("tt", "ti", "it", "ii")}, dict(Q=Q, KV=KV, st=st, Hs=Hs, HP=HP, Es=Es,
+                                                                         EP=EP)
 
 
 def _bwd_two_streams(ctx, cfg, dS, state, need_dX, need_e, outs):
@@ -354,10 +390,11 @@ def head_forward(ctx, cfg: HeadConfig, X_t, X_i, E_t, E_i):
     if two:
         Hs, rst, S, cst = _fwd_two_streams(ctx, cfg, {"text": X_t, "image": X_i}, Es)
     else:
+        HP = {}
         for m, x in (("text", X_t), ("image", X_i)):
             if x is not None:
-                Hs[m], rst[m] = _repr_modality_fwd(ctx, cfg, x, m, unimodal=uni)
-        S, cst = _cond_fwd(ctx, cfg, Hs, Es)
+                Hs[m], HP[m], rst[m] = _repr_modality_fwd(ctx, cfg, x, m, unimodal=uni)
+        S, cst = _cond_fwd(ctx, cfg, Hs, HP, Es)
     pooled, hst, outs = {}, {}, {}
     if cfg.text_only:
         p = K.seq_mean_fwd(S["tt"])
