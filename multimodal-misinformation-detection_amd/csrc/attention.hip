@@ -47,6 +47,7 @@ struct AttnP {
   // fp32 backward: split planes of the packed [dq | dk | dv] buffer (base = dq), see mmfd_attn_args
   bf16* pl; int64_t pl_stride; const float* pl_base; int pl_only;
   int idx32;  // every dropout index fits 32 bits (hash_c1)
+  int vst;    // x6 backward stores as 4-column groups (16-B fp32, 8-B planes): outputs and planes aligned
   int dbg;  // x6 phase experiments (MMFD_X6A_DBG): 1 = stage zeros, 2 = skip the products
 };
 
@@ -66,6 +67,55 @@ __device__ __forceinline__ void plane_put(const AttnP& p, const float* dst, floa
 // Lk * C1 per query — so an element costs one v_add in place of the 64-bit index arithmetic and
 // its two extra 32-bit multiplies (bit-identical masks).
 constexpr uint32_t HASH_C1 = 0x9e3779b1u;
+
+// 4x4 transpose across each lane quad (lanes 4j + t): afterwards lane t, register c holds what lane
+// c held in register t. A 16x16 MFMA accumulator (lane (g, i): rows 4g + r, column i) becomes
+// rows 4g + (i & 3) with 4 consecutive columns 4 (i >> 2) + c per lane — one 16-B fp32 store and
+// 8-B plane stores per 4 outputs instead of one 4-B and three 2-B stores per output
+__device__ __forceinline__ void quad_tr(float (&x)[4], int t) {
+  const bool o1 = t & 1, o2 = t & 2;
+#pragma unroll
+  for (int j = 0; j < 4; j += 2) {
+    const float r = __shfl_xor(o1 ? x[j] : x[j + 1], 1, 64);
+    if (o1) x[j] = r; else x[j + 1] = r;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float r = __shfl_xor(o2 ? x[j] : x[j + 2], 2, 64);
+    if (o2) x[j] = r; else x[j + 2] = r;
+  }
+}
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+// four consecutive fp32 outputs at dst (16-B aligned; AttnP::vst), accumulated onto dst when acc,
+// and their split planes when p.pl (the same split3 rule as plane_put)
+__device__ __forceinline__ void x6_put4(const AttnP& p, float* dst, const float (&x)[4], bool acc) {
+  float4 v = make_float4(x[0], x[1], x[2], x[3]);
+  if (acc) {
+    const float4 o = *reinterpret_cast<const float4*>(dst);
+    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+  }
+  if (p.pl) {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    bf16x4 h, m, l;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bf16 hu = (bf16)e[u];
+      const float r = e[u] - (float)hu;
+      const bf16 mu = (bf16)r;
+      h[u] = hu;
+      m[u] = mu;
+      l[u] = (bf16)(r - (float)mu);
+    }
+    bf16* pp = p.pl + (dst - p.pl_base);
+    *reinterpret_cast<uint2*>(pp) = __builtin_bit_cast(uint2, h);
+    *reinterpret_cast<uint2*>(pp + p.pl_stride) = __builtin_bit_cast(uint2, m);
+    *reinterpret_cast<uint2*>(pp + 2 * p.pl_stride) = __builtin_bit_cast(uint2, l);
+    if (p.pl_only) return;
+  }
+  *reinterpret_cast<float4*>(dst) = v;
+}
 __device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
 
 template <typename T, int D>
@@ -1675,6 +1725,25 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   };
   auto kstore = [&](int kbk, const f32x4 (&dkv)[2 * DT]) {
     const int64_t k0 = (int64_t)kbk * 16;
+    if (p.vst) {  // (uniform) quad transposes, then 4-column stores
+      const int t = li & 3, c4 = 4 * (li >> 2);
+      const int64_t key = k0 + 4 * g + t;
+      float* krow = dkb + key * p.dk_st + c4;
+      float* vrow = dvb + key * p.dv_st + c4;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        float xk[4] = {dkv[2 * d + 1][0] * p.scale, dkv[2 * d + 1][1] * p.scale, dkv[2 * d + 1][2] * p.scale,
+                       dkv[2 * d + 1][3] * p.scale};
+        float xv[4] = {dkv[2 * d][0], dkv[2 * d][1], dkv[2 * d][2], dkv[2 * d][3]};
+        quad_tr(xk, t);
+        quad_tr(xv, t);
+        if (key < p.Lk && d * 16 + c4 < p.D) {
+          x6_put4(p, krow + d * 16, xk, p.acc_dkv);
+          x6_put4(p, vrow + d * 16, xv, p.acc_dkv);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t key = k0 + 4 * g + r;
@@ -1875,6 +1944,18 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   };
   auto qstore = [&](int qbk, const f32x4 (&dq)[DT]) {
     const int64_t q0 = (int64_t)qbk * 16;
+    if (p.vst) {  // (uniform) quad transposes, then 4-column stores
+      const int t = li & 3, c4 = 4 * (li >> 2);
+      const int64_t q = q0 + 4 * g + t;
+      float* qrow = dqb + q * p.dq_st + c4;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        float x[4] = {dq[d][0] * p.scale, dq[d][1] * p.scale, dq[d][2] * p.scale, dq[d][3] * p.scale};
+        quad_tr(x, t);
+        if (q < p.Lq && d * 16 + c4 < p.D) x6_put4(p, qrow + d * 16, x, p.acc_dq);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t q = q0 + 4 * g + r;
@@ -2029,6 +2110,13 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.delta = a.delta;
   p.acc_dq = a.accumulate_dq; p.acc_dkv = a.accumulate_dkv;
   p.idx32 = (uint64_t)a.B * (uint64_t)a.H * (uint64_t)a.Lq * (uint64_t)a.Lk <= (1ull << 32);
+  auto al4 = [](const void* ptr, int64_t sb, int64_t st) {
+    return ptr && ((uintptr_t)ptr & 15) == 0 && sb % 4 == 0 && st % 4 == 0;
+  };
+  // (the forward keeps its per-element stores: the 4-column form measured 2-8 % slower there)
+  p.vst = a.dtype == MMFD_F32 && bwd && al4(a.dq, a.dq_sb, a.dq_st) && al4(a.dk, a.dk_sb, a.dk_st) &&
+          al4(a.dv, a.dv_sb, a.dv_st);
+  p.pl = nullptr; p.pl_only = 0;
   static const int dbg = getenv("MMFD_X6A_DBG") ? atoi(getenv("MMFD_X6A_DBG")) : 0;
   p.dbg = dbg;
   return 0;
@@ -2170,6 +2258,7 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
                    "attn_bwd: planes_only excludes accumulate");
     if (v2) {  // the v2 kernels write the planes from their stores
       p.pl = (bf16*)a->dqkv_planes; p.pl_stride = p.B * p.Lq * W; p.pl_base = (const float*)a->dq;
+      if ((uintptr_t)p.pl & 7) p.vst = 0;
       p.pl_only = a->planes_only;
     }
   }

@@ -1,6 +1,6 @@
 """Attention kernels at the encoder shapes (bs=256 pairs -> 512 sequences x 12 heads, D=64):
 BERT L=128 with key mask + dropout 0.1, ViT L=197 without. Prints per-kernel-call times.
-python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native]"""
+python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native] [--planes]"""
 import argparse
 import os
 import sys
@@ -12,7 +12,7 @@ import mmfd  # noqa: E402
 from mmfd import kernels as K  # noqa: E402
 
 
-def case(name, L, masked, p, iters, dtype=torch.bfloat16):
+def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False):
     B, H, D = 512, 12, 64
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -28,17 +28,25 @@ def case(name, L, masked, p, iters, dtype=torch.bfloat16):
     kw = dict(key_bias=kb, dropout_p=p, seed=seed, salt=K.salt_of("bench")) if p > 0 else dict(key_bias=kb)
     o, lse = K.attn_fwd(q, k, v, H, **kw)
     dq = torch.empty_like(q); dk = torch.empty_like(k); dv = torch.empty_like(v)
+    fkw, bkw = {}, {}
+    if planes and dtype == torch.float32:
+        # as the fp32 encoders run it: the output's planes from the forward, the packed dq|dk|dv
+        # written as planes only by the backward
+        fkw = dict(o_planes=torch.empty(3, B * L, H * D, device=dev, dtype=torch.bfloat16))
+        dqkv = torch.empty(B, L, 3 * H * D, device=dev, dtype=dtype)
+        dq, dk, dv = dqkv[..., :H * D], dqkv[..., H * D:2 * H * D], dqkv[..., 2 * H * D:]
+        bkw = dict(dqkv_planes=torch.empty(3, B * L, 3 * H * D, device=dev, dtype=torch.bfloat16), planes_only=True)
     for _ in range(2):
-        K.attn_fwd(q, k, v, H, out=o, **kw)
-        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw)
+        K.attn_fwd(q, k, v, H, out=o, **kw, **fkw)
+        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw, **bkw)
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     tf = tb = 0.0
     for _ in range(iters):
         ev[0].record()
-        K.attn_fwd(q, k, v, H, out=o, **kw)
+        K.attn_fwd(q, k, v, H, out=o, **kw, **fkw)
         ev[1].record()
-        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw)
+        K.attn_bwd(q, k, v, o, lse, dout, H, dq=dq, dk=dk, dv=dv, **kw, **bkw)
         ev[2].record()
         torch.cuda.synchronize()
         tf += ev[0].elapsed_time(ev[1])
@@ -55,11 +63,12 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     ap.add_argument("--dtype", default="bf16,fp32")
     ap.add_argument("--fp32-mode", default="split", help="fp32 attention: split (bf16 planes) or native")
+    ap.add_argument("--planes", action="store_true", help="fp32: output / gradient planes as the encoders use them")
     a = ap.parse_args()
     K.set_fp32_attn_mode(a.fp32_mode)
     for dt in a.dtype.split(","):
         t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
         if a.only in ("", "bert"):
-            case(f"{dt} bert L=128 mask+drop", 128, True, 0.1, a.iters, t)
+            case(f"{dt} bert L=128 mask+drop", 128, True, 0.1, a.iters, t, a.planes)
         if a.only in ("", "vit"):
-            case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t)
+            case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t, a.planes)
