@@ -587,7 +587,9 @@ int choose_splits(const mmfd_gemm_args& a, int64_t* ws_bytes_needed, bool x6 = f
       // modelled time (us): rounds of 256 blocks x (K-tiles per block x ~1.8 us + ~3 us block
       // overhead) + the fp32 slab round trip (written by the blocks, read by the reduce) at ~5 TB/s
       double best = 1e30;
-      const int smax = (int)std::min<int64_t>(32, nkt / 8);
+      // (up to one round of blocks: the fusion head's 256x256 weight gradients over 32k-50k rows are
+      // a single tile, and 32 splits left 224 CUs idle for ~180 us per launch)
+      const int smax = (int)std::min<int64_t>(std::max<int64_t>(32, 256 / tiles), nkt / 8);
       // one 256x256 K-tile (bf16 / fp32 MFMA rate; a fused split-operand step = 3 bf16 K-tiles of MFMA)
       const double kt_us = xf ? 3.6 : (a.dtype == MMFD_BF16 || x6) ? 1.8 : 7.0;
       for (int sp = 1; sp <= smax; ++sp) {

@@ -701,3 +701,27 @@ def test_attention_fwd_output_planes(L):
     torch.cuda.synchronize()
     assert torch.equal(o0, o1) and torch.equal(l0, l1)
     assert torch.equal(pl.view(torch.int16), K.split3(o1.view(B * L, -1)).view(torch.int16))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_single_tile_weight_gradient_many_splits(dtype):
+    """the fusion head's weight-gradient shape (256 x 256 over 50,432 rows): one output tile, split-K
+    up to one round of blocks (more than the former cap of 32 splits), with the fused bias gradient
+    accumulating onto a shared parameter's first use"""
+    from mmfd.kernels import GemmArgs, dtype_code, lib
+    import ctypes
+    Kd, M, N = 50432, 256, 256
+    dy = _rand(Kd, M, dtype=dtype, seed=71).to(DEV); xx = _rand(Kd, N, dtype=dtype, seed=72).to(DEV)
+    a = GemmArgs()
+    a.dtype, a.c_dtype = dtype_code(dtype), dtype_code(torch.float32)
+    a.trans_a, a.trans_b = 1, 1
+    a.M, a.N, a.K = M, N, Kd
+    a.A, a.lda, a.B, a.ldb = dy.data_ptr(), M, xx.data_ptr(), N
+    assert lib().mmfd_gemm_splits(ctypes.byref(a)) > 32
+    rs = torch.full((M,), 0.25, device=DEV)
+    dw = K.gemm(dy, xx, trans_a=True, trans_b=True, out_dtype=torch.float32, a_rowsum=rs, a_rowsum_beta=1.0)
+    torch.cuda.synchronize()
+    ref = dy.double().T @ xx.double()
+    tol = (1e-5 if dtype == torch.float32 else 2e-3) * ref.abs().max().item()
+    assert (dw.double() - ref).abs().max().item() <= tol
+    assert (rs.double() - (0.25 + dy.double().sum(0))).abs().max().item() <= 1e-4 * math.sqrt(Kd)
