@@ -885,6 +885,9 @@ def train_leg(args, dev, world, rank, precision):
     # duration by the CUs the other stream holds — the roofline is a property of the kernel alone
     steps_in_prof = 2
     conc, tr.concurrent = tr.concurrent, False
+    # (the fusion head's claim-text / claim-image halves likewise on one stream, fusion._two_streams)
+    serial_head = os.environ.get("MMFD_SERIAL_HEAD")
+    os.environ["MMFD_SERIAL_HEAD"] = "1"
     if graphed:  # the graph's private pool would double the eager probe's footprint
         tr.release_graph()
     # one untimed eager step first: it refills the caching allocator (the hipMallocs of a cold pool
@@ -895,6 +898,10 @@ def train_leg(args, dev, world, rank, precision):
         for _ in range(steps_in_prof):
             tr.step(batch)
     tr.concurrent = conc
+    if serial_head is None:
+        del os.environ["MMFD_SERIAL_HEAD"]
+    else:
+        os.environ["MMFD_SERIAL_HEAD"] = serial_head
     prof = probe.summary()
     dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     # achieved = algorithmic FLOPs (2MNK per launch) / measured launch time. The split-operand fp32
