@@ -383,7 +383,23 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, T
   if (e.vec && (N % 8) == 0) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total / 8; g += (int64_t)gridDim.x * blockDim.x) {
       float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < splits; ++s) {
+      int s = 0;
+      // four slabs' loads in flight before their adds (the adds stay in split order: same sums)
+      for (; s + 4 <= splits; s += 4) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* p = ws + (int64_t)(s + u) * total + g * 8;
+          a[u] = *reinterpret_cast<const float4*>(p);
+          b[u] = *reinterpret_cast<const float4*>(p + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          z[0] += a[u].x; z[1] += a[u].y; z[2] += a[u].z; z[3] += a[u].w;
+          z[4] += b[u].x; z[5] += b[u].y; z[6] += b[u].z; z[7] += b[u].w;
+        }
+      }
+      for (; s < splits; ++s) {
         const float* p = ws + (int64_t)s * total + g * 8;
         const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
         z[0] += a.x; z[1] += a.y; z[2] += a.z; z[3] += a.w; z[4] += b.x; z[5] += b.y; z[6] += b.z; z[7] += b.w;
