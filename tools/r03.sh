@@ -12,3 +12,4 @@ MMFD_SERIAL_ENCODERS=1 MMFD_SERIAL_HEAD=1 BENCH_ARGS="--precision fp32 --no-bf16
 PMC=0 STEPS=4 BENCH_ARGS="--precision fp32 --no-bf16" bash tools/profile.sh ${T}_fp32_step
 MMFD_SERIAL_ENCODERS=1 MMFD_SERIAL_HEAD=1 STEPS=4 BENCH_ARGS="--precision bf16 --no-bf16" bash tools/profile.sh ${T}_bf16
 python3 tools/pmc_mfma_summary.py gpurun_out/prof_${T}_fp32 ${T}_fp32
+MMFD_SERIAL_ENCODERS=1 MMFD_SERIAL_HEAD=1 BENCH_ARGS="--precision bf16 --no-bf16" bash tools/pmc_mfma.sh ${T}_bf16
