@@ -64,11 +64,12 @@ if __name__ == "__main__":
     ap.add_argument("--dtype", default="bf16,fp32")
     ap.add_argument("--fp32-mode", default="split", help="fp32 attention: split (bf16 planes) or native")
     ap.add_argument("--planes", action="store_true", help="fp32: output / gradient planes as the encoders use them")
+    ap.add_argument("--bert-p", type=float, default=0.1, help="BERT case dropout probability")
     a = ap.parse_args()
     K.set_fp32_attn_mode(a.fp32_mode)
     for dt in a.dtype.split(","):
         t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
         if a.only in ("", "bert"):
-            case(f"{dt} bert L=128 mask+drop", 128, True, 0.1, a.iters, t, a.planes)
+            case(f"{dt} bert L=128 mask p={a.bert_p}", 128, True, a.bert_p, a.iters, t, a.planes)
         if a.only in ("", "vit"):
             case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t, a.planes)
