@@ -310,13 +310,19 @@ class ImageCorpus:
     pickle (path -> fp32 [2048] tensor) unless its name ends in .npz (`paths`, `features`)."""
 
     def __init__(self, feature_corpus_path, extractor: ImageSimilarity | None = None, batch_size=256,
-                 decode_workers=None):
+                 decode_workers=None, decode="processes"):
         self.feature_corpus_path = feature_corpus_path
         self.feature_extractor = extractor or ImageSimilarity()
         self.batch_size = batch_size
-        # host decode threads (PIL releases the GIL while it decodes): the next batch is decoded
-        # while the GPU preprocesses and embeds the current one
+        # host decode workers: the next batch is decoded while the GPU preprocesses and embeds the
+        # current one. "processes" (default): a forkserver process pool handing the pixels back in
+        # shared memory (mmfd.hostdecode; PIL holds the GIL outside its decoder, which capped the
+        # thread pool at ~1.6k images/s); "threads": the thread pool of round 3
         self.decode_workers = decode_workers or min(16, len(os.sched_getaffinity(0)))
+        if decode not in ("processes", "threads"):
+            raise ValueError("decode must be 'processes' or 'threads'")
+        self.decode = decode
+        self._pool = None
         self.feature_dict = self.load_features()
         self._revision = 0  # bumped on every feature_dict write: the device index is rebuilt
 
@@ -351,12 +357,38 @@ class ImageCorpus:
         self._revision += 1
         self.save_features()
 
+    def _decode_pool(self):
+        if self._pool is None:
+            from .hostdecode import DecodePool
+            self._pool = DecodePool(self.decode_workers)
+        return self._pool
+
+    def close(self):
+        """stop the decode worker processes (they are otherwise kept for the next build)"""
+        if self._pool is not None:
+            self._pool.close()
+            self._pool = None
+
     def _extract_paths(self, paths):
-        from concurrent.futures import ThreadPoolExecutor
         out = {}
         chunks = [paths[i:i + self.batch_size] for i in range(0, len(paths), self.batch_size)]
         if not chunks:
             return out
+        if self.decode == "processes" and self.decode_workers > 1:
+            pool = self._decode_pool()
+            nxt = pool.submit(chunks[0])
+            for ci, chunk in enumerate(chunks):
+                imgs, release = pool.get(nxt)
+                if ci + 1 < len(chunks):  # decode the next batch on the host while this one runs
+                    nxt = pool.submit(chunks[ci + 1])
+                px = self.feature_extractor.preprocess_batch(imgs)  # copies the pixels (pinned upload)
+                del imgs
+                release()
+                feats = self.feature_extractor.extract_batch(px).float().cpu()
+                for p, f in zip(chunk, feats):
+                    out[p] = f.clone()
+            return out
+        from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(max_workers=max(1, self.decode_workers)) as pool:
             nxt = [pool.submit(_decode, p) for p in chunks[0]]
             for ci, chunk in enumerate(chunks):

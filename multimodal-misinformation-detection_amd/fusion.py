@@ -161,6 +161,16 @@ def _head_stream(device):
     return s
 
 
+def _publish(stream, *ts):
+    """mark tensors one head stream hands to the other as used by `stream` (record_stream), so the
+    caching allocator does not give their blocks to a later allocation of the producing stream
+    before the reader's queued kernels have run. (The side stream also always starts with
+    side.wait_stream(main), ADVICE r3: this keeps the hand-off safe without relying on that.)"""
+    for t in ts:
+        if torch.is_tensor(t):
+            t.record_stream(stream)
+
+
 def _event():
     e = torch.cuda.Event()
     e.record()
@@ -300,9 +310,8 @@ def _fwd_two_streams(ctx, cfg, Xs, Es):
                 path = PATH_OF[(m, em)]
                 out[path[2]], st[path[2]] = _path_fwd(ctx, cfg, path, Q[m], KV[em], Hs[m])
     main.wait_stream(side)
-    # (every tensor one stream reads from the other stays referenced by the head state until the
-    # backward has joined both streams again, so the caching allocator cannot hand its memory to
-    # the producing stream while the reader may still be queued)
+    _publish(side, KV["text"])
+    _publish(main, KV["image"], out["it"], out["ii"], Hs["image"])
     return Hs, rst, {t: out[t] for t in ("tt", "ti", "it", "ii")}, dict(Q=Q, KV=KV, st=st, Hs=Hs, HP=HP, Es=Es,
                                                                          EP=EP)
 
@@ -316,6 +325,7 @@ def _bwd_two_streams(ctx, cfg, dS, state, need_dX, need_e, outs):
     main = torch.cuda.current_stream()
     side = _head_stream(dS["tt"].device)
     side.wait_stream(main)
+    _publish(side, dS["it"], dS["ii"])
     streams = {"text": main, "image": side}
     dKVs, ev, dX, dE = {}, {}, {}, {}
     for m in ("text", "image"):
@@ -336,6 +346,8 @@ def _bwd_two_streams(ctx, cfg, dS, state, need_dX, need_e, outs):
             K.axpby(1.0, dKVs["text"][em], 1.0, dKVs["image"][em], out=dkv)
             dE[em] = _kv_bwd(ctx, cfg, em, dkv, cst, need_e[em], outs["E" + em])
     main.wait_stream(side)
+    _publish(side, dKVs["text"].get("image"))
+    _publish(main, dKVs["image"].get("text"), dX.get("image"), dE.get("image"))
     return dX, dE
 
 

@@ -33,7 +33,7 @@ import os
 
 import torch
 
-from .train import FusionTrainer
+from .train import FusionTrainer, load_checkpoint
 
 logger = logging.getLogger(__name__)
 
@@ -239,7 +239,7 @@ class MisinformationPredictor:
             num_heads=num_heads, dropout=dropout, hidden_dim=hidden_dim, num_classes=num_classes,
             mlp_ratio=mlp_ratio, fused_attn=fused_attn).to(self.device)
         logger.info(f"Loading model from {model_path}")
-        checkpoint = torch.load(model_path, map_location="cpu", weights_only=True)
+        checkpoint = load_checkpoint(model_path)
         self.model.load_state_dict(checkpoint["model_state_dict"])
         for m in (self.text_encoder, self.image_encoder, self.model):
             m.set_precision(precision)

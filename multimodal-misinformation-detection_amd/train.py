@@ -64,6 +64,26 @@ def category_loss(pred, labels):
     return _XentFn.apply(labels.reshape(-1), (0,), pred)
 
 
+def _numpy_scalar_globals():
+    """the pickle globals a numpy scalar needs (np.float64 / np.int64 as np.mean and sklearn leave
+    them): the scalar reconstructor under its numpy-2 and numpy-1 module paths and the dtype classes"""
+    import numpy as np
+    scalar = np._core.multiarray.scalar
+    allow = [scalar, (scalar, "numpy.core.multiarray.scalar"), np.dtype]
+    for t in (np.float64, np.float32, np.float16, np.int64, np.int32, np.bool_):
+        allow.append(type(np.dtype(t)))
+    return allow
+
+
+def load_checkpoint(path, map_location="cpu"):
+    """torch.load(weights_only=True) of a reference checkpoint. The reference's best_model.pt
+    (train.py:413-428) stores the best metric as a numpy scalar (np.mean of the F1s), which the
+    weights-only unpickler refuses by default: only numpy's scalar reconstructor and dtype classes
+    are allowed in addition — still no code from the file runs."""
+    with torch.serialization.safe_globals(_numpy_scalar_globals()):
+        return torch.load(path, map_location=map_location, weights_only=True)
+
+
 class FusionTrainer:
     """Encoders + fusion head + AdamW as one training step (train.py:123-188).
 
@@ -199,9 +219,10 @@ class FusionTrainer:
         a HIP graph: replay() then runs it with one launch and no per-kernel host work (the dropout
         seeds advance on the device, AdamW's pointer table is bound after capture). `batch` tensors
         are the graph's static inputs: refill them in place (or pass a batch to replay) between
-        replays. Single process only (the DP all-reduce stays eager)."""
-        if self.dp is not None:
-            raise RuntimeError("capture(): the data-parallel step runs eagerly")
+        replays. With data parallelism (`dp`) the gradient all-reduce is captured too: the per-
+        stream bucket packs, the RCCL all_reduce kernels (ProcessGroupNCCL keeps captured work out of
+        its watchdog) and finish()'s wait + unpack become nodes of the same graph; the buckets were
+        allocated by the eager warm-up steps, so the graph reads and writes fixed addresses."""
         self._static = batch
         s = torch.cuda.Stream(device=self._device())
         s.wait_stream(torch.cuda.current_stream())
@@ -263,8 +284,9 @@ def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders
     """bert-base-uncased + ViT-B/16 + the fusion head at 768/768 (BASELINE configs 2-4), random init
     from `seed` (the same on every rank; with `dp` rank 0's weights are broadcast anyway); the
     dropout streams are offset per rank so replicas draw independent masks. `dropout` is the head's
-    (model.py dropout=0.1); the encoders keep their HF configs' own (BERT 0.1, ViT 0.0) unless
-    `encoder_dropout` overrides both."""
+    (model.py dropout=0.1); the encoders keep their HF configs' own (BERT 0.1, ViT 0.0).
+    `encoder_dropout` overrides BERT's only: ViT-B/16 trains without dropout, and mmfd's ViT
+    implements only that configuration (a ViTConfig with dropout raises in training)."""
     torch.manual_seed(seed)
     bc = BertConfig() if encoder_dropout is None else BertConfig(hidden_dropout_prob=encoder_dropout,
                                                                   attention_probs_dropout_prob=encoder_dropout)
@@ -432,7 +454,7 @@ def main(args):
                                         hidden_dim=args.hidden_dim, num_classes=args.num_classes,
                                         mlp_ratio=args.mlp_ratio, fused_attn=args.fused_attn)
     if args.init_checkpoint:
-        ck = torch.load(args.init_checkpoint, map_location="cpu", weights_only=True)
+        ck = load_checkpoint(args.init_checkpoint)
         head.load_state_dict(ck.get("model_state_dict", ck))
     head = head.to(device)
     head.manual_seed(args.seed + 7919 * rank)

@@ -79,3 +79,40 @@ class OracleTrainer:
         total.backward()
         self.opt.step()
         return total.detach(), [p.detach() for p in per]
+
+
+def chunked_loss_grads(bert_p, vit_p, head_p, batch, *, bert_cfg=BERT_BASE, vit_cfg=VIT_B16, num_heads=8, chunk=8,
+                       drop=None, progress=None):
+    """The loss and parameter gradients of ONE step on a large batch (train.py:146-170 with
+    trainable encoders: Σ over the 4 paths of the batch-mean cross-entropy), computed in chunks of
+    `chunk` pairs so the CPU autograd graph stays small: chunk c contributes n_c / B of its own
+    mean loss, so the accumulated gradients are those of the whole-batch mean. Returns
+    (total, [4 path losses], {"bert."/"vit."/"head." + name: grad})."""
+    bp = {k: v.clone().float().requires_grad_(True) for k, v in bert_p.items()}
+    vp = {k: v.clone().float().requires_grad_(True) for k, v in vit_p.items()}
+    hp = {k: v.clone().float().requires_grad_(True) for k, v in head_p.items()}
+    B = batch["labels"].shape[0]
+    total = torch.zeros((), dtype=torch.float64)
+    per = torch.zeros(4, dtype=torch.float64)
+    for s in range(0, B, chunk):
+        e = min(B, s + chunk)
+        n = e - s
+        ids = torch.cat([batch["input_ids"][s:e], batch["input_ids"][B + s:B + e]])
+        mask = torch.cat([batch["attention_mask"][s:e], batch["attention_mask"][B + s:B + e]])
+        px = torch.cat([batch["pixel_values"][s:e], batch["pixel_values"][B + s:B + e]])
+        T = OE.bert_forward(bp, ids, mask, None, num_layers=bert_cfg["num_hidden_layers"],
+                            num_heads=bert_cfg["num_attention_heads"], drop=drop)
+        I = OE.vit_forward(vp, px, num_layers=vit_cfg["num_hidden_layers"],
+                           num_heads=vit_cfg["num_attention_heads"], patch=vit_cfg["patch_size"])
+        out = OF.model_forward(hp, T[:n], I[:n], T[n:], I[n:], num_heads=num_heads, drop=drop)
+        t, pl = OF.path_loss(out, batch["labels"][s:e])
+        (t * (n / B)).backward()
+        total += t.detach().double() * (n / B)
+        per += torch.stack([p.detach().double() for p in pl]) * (n / B)
+        if progress is not None:
+            progress(e, B)
+    grads = {}
+    for pre, d in (("bert.", bp), ("vit.", vp), ("head.", hp)):
+        for k, p in d.items():
+            grads[pre + k] = None if p.grad is None else p.grad.detach()
+    return total, list(per), grads

@@ -36,8 +36,9 @@ def tiny_batch(B, cfg=TINY, seed=0, ragged=True):
     return {"input_ids": ids, "attention_mask": mask, "pixel_values": px, "labels": labels}
 
 
-def build_pair(precision="fp32", dropout=0.1, cfg=TINY, seed=5, lr=1e-3):
-    """(HIP FusionTrainer on cuda:0, OracleTrainer on CPU) with identical initial weights and dropout masks."""
+def build_modules(dropout=0.1, cfg=TINY, seed=5):
+    """(text, image, head) mmfd modules on the CPU from `seed`, and their initial state_dicts
+    (the weights the oracle starts from; tests/golden/make_config3_bs256.py uses the same recipe)."""
     torch.manual_seed(seed)
     bc = BertConfig(vocab_size=cfg["vocab"], hidden_size=cfg["D"], num_hidden_layers=cfg["layers"],
                     num_attention_heads=cfg["heads"], intermediate_size=cfg["inter"],
@@ -49,13 +50,26 @@ def build_pair(precision="fp32", dropout=0.1, cfg=TINY, seed=5, lr=1e-3):
     head = MisinformationDetectionModel(text_input_dim=cfg["D"], image_input_dim=cfg["D"], embed_dim=cfg["embed"],
                                         num_heads=cfg["head_heads"], dropout=dropout, hidden_dim=cfg["hidden"])
     states = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in (text, image, head)]
+    return text, image, head, states
+
+
+def oracle_cfgs(cfg):
+    bcfg = dict(hidden_size=cfg["D"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"])
+    vcfg = dict(patch_size=cfg["patch"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"])
+    return bcfg, vcfg
+
+
+def build_pair(precision="fp32", dropout=0.1, cfg=TINY, seed=5, lr=1e-3, with_oracle=True):
+    """(HIP FusionTrainer on cuda:0, OracleTrainer on CPU) with identical initial weights and dropout masks."""
+    text, image, head, states = build_modules(dropout, cfg, seed)
     dev = torch.device("cuda", 0)
     text, image, head = text.to(dev), image.to(dev), head.to(dev)
     text.manual_seed(99)
     head.manual_seed(99)  # same seed: every dropout site has its own salt
     tr = FusionTrainer(text, image, head, lr=lr, precision=precision)
-    bcfg = dict(hidden_size=cfg["D"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"])
-    vcfg = dict(patch_size=cfg["patch"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"])
+    if not with_oracle:
+        return tr, states
+    bcfg, vcfg = oracle_cfgs(cfg)
     ref = OracleTrainer(*states, bert_cfg=bcfg, vit_cfg=vcfg, num_heads=cfg["head_heads"], lr=lr,
                         drop=make_drop(99, dropout) if dropout > 0 else None)
     return tr, ref

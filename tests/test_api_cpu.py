@@ -252,3 +252,52 @@ def test_checked_state_dict_load():
         load_state_dict_checked(m, dict(sd, extra=torch.zeros(1)))
     with pytest.raises(RuntimeError, match="missing"):
         load_state_dict_checked(m, {k: v for k, v in sd.items() if k != "1.bias"})
+
+
+def _rewrite_pickle_module(raw: bytes, old: bytes, new: bytes) -> bytes:
+    """the same torch.save archive with a pickle global's module path renamed (simulates a
+    checkpoint written under numpy 1.x, whose scalars pickle as numpy.core.multiarray.scalar)"""
+    import io
+    import zipfile
+    src, dst = zipfile.ZipFile(io.BytesIO(raw)), io.BytesIO()
+    with zipfile.ZipFile(dst, "w", compression=zipfile.ZIP_STORED) as z:
+        for info in src.infolist():
+            data = src.read(info.filename)
+            if info.filename.endswith("data.pkl"):
+                assert old in data
+                data = data.replace(old, new)
+            z.writestr(info, data)
+    return dst.getvalue()
+
+
+@pytest.mark.parametrize("numpy1", [False, True])
+def test_best_model_checkpoint_with_numpy_metric_loads(tmp_path, numpy1):
+    """the reference's best_model.pt (train.py:413-428) holds the best metric as a numpy
+    scalar (np.mean of F1s) next to model_state_dict / optimizer_state_dict; mmfd's weights-only
+    loader (MisinformationPredictor, --init_checkpoint) must read it, and still refuse other globals."""
+    import io
+
+    from mmfd.train import load_checkpoint
+    m = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, hidden_dim=16)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+    ck = {"epoch": 3, "global_step": np.int64(1200), "model_state_dict": m.state_dict(),
+          "optimizer_state_dict": opt.state_dict(), "avg_f1": np.mean(np.array([0.5, 0.7, 0.6]))}
+    buf = io.BytesIO()
+    torch.save(ck, buf)
+    raw = buf.getvalue()
+    if numpy1:
+        raw = _rewrite_pickle_module(raw, b"numpy._core.multiarray", b"numpy.core.multiarray")
+    path = tmp_path / "best_model.pt"
+    path.write_bytes(raw)
+    with pytest.raises(Exception):
+        torch.load(path, map_location="cpu", weights_only=True)  # the plain loader refuses it
+    got = load_checkpoint(path)
+    assert float(got["avg_f1"]) == pytest.approx(0.6) and int(got["global_step"]) == 1200
+    m2 = MisinformationDetectionModel(text_input_dim=48, image_input_dim=40, embed_dim=32, num_heads=4, hidden_dim=16)
+    m2.load_state_dict(got["model_state_dict"])
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, m2.state_dict()[k])
+    bad = tmp_path / "bad.pt"  # any other global still refuses
+    torch.save({"model_state_dict": m.state_dict(), "x": io.BytesIO}, bad)
+    with pytest.raises(Exception):
+        load_checkpoint(bad)

@@ -25,7 +25,9 @@ class _StubExtractor:
         from oracle.preprocess import preprocess
         from mmfd.preprocess import MODES
         c = MODES["retrieval"]
-        return torch.stack([torch.from_numpy(preprocess(im, c["resize"], None, c["mean"], c["std"])) for im in images])
+        from PIL import Image
+        ims = [Image.fromarray(im) if isinstance(im, np.ndarray) else im for im in images]
+        return torch.stack([torch.from_numpy(preprocess(im, c["resize"], None, c["mean"], c["std"])) for im in ims])
 
     def extract_batch(self, px):
         return torch.cat([px.mean(dim=(2, 3)), px.amax(dim=(2, 3))], dim=1)
@@ -148,3 +150,60 @@ def test_sharded_text_corpus_equals_single_process(tmp_path):
     e2, i2 = TextCorpus.read(str(tmp_path / "sharded" / os.path.basename(one)))
     assert i1 == i2 == [f"train_{i}" for i in range(11)]
     assert e1.dtype == np.float16 and np.array_equal(e1, e2)
+
+
+def test_process_pool_decode_is_bit_exact(tmp_path):
+    """mmfd.hostdecode.DecodePool (worker processes, pixels returned in shared memory) returns exactly
+    the bytes of evidence._decode (PIL open + convert("RGB")) for JPEG / PNG / grayscale / RGBA /
+    palette files, in submission order, and leaves no shared-memory block behind."""
+    from PIL import Image
+
+    from mmfd.evidence import _decode
+    from mmfd.hostdecode import DecodePool
+    rng = np.random.default_rng(7)
+    paths = []
+    for i, (mode, ext) in enumerate([("RGB", "jpg"), ("RGB", "png"), ("L", "jpg"), ("RGBA", "png"), ("P", "png"),
+                                     ("RGB", "jpeg"), ("L", "png")] * 3):
+        h, w = 17 + 5 * i, 23 + 3 * i
+        a = rng.integers(0, 255, (h, w, 4 if mode == "RGBA" else 3), dtype=np.uint8)
+        im = Image.fromarray(a, "RGBA" if mode == "RGBA" else "RGB")
+        if mode in ("L", "P"):
+            im = im.convert(mode)
+        p = str(tmp_path / f"x{i:02d}.{ext}")
+        im.save(p)
+        paths.append(p)
+    shm_before = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
+    pool = DecodePool(workers=3, group=4)
+    try:
+        h1 = pool.submit(paths[:10])
+        h2 = pool.submit(paths[10:])
+        for h, ps in ((h1, paths[:10]), (h2, paths[10:])):
+            views, release = pool.get(h)
+            assert len(views) == len(ps)
+            for v, p in zip(views, ps):
+                want = np.asarray(_decode(p))
+                assert v.dtype == np.uint8 and v.shape == want.shape and np.array_equal(v, want), p
+            del v, views
+            release()
+        with pytest.raises(Exception):
+            pool.get(pool.submit([str(tmp_path / "missing.jpg")]))
+    finally:
+        pool.close()
+    if shm_before or os.path.isdir("/dev/shm"):
+        assert set(os.listdir("/dev/shm")) - shm_before == set()
+
+
+def test_corpus_decode_processes_equals_threads(tmp_path):
+    from mmfd.evidence import ImageCorpus
+    os.makedirs(tmp_path / "imgs")
+    _images(str(tmp_path / "imgs"), n=9)
+    a = ImageCorpus(str(tmp_path / "p.pkl"), extractor=_StubExtractor(), batch_size=4, decode_workers=3)
+    b = ImageCorpus(str(tmp_path / "t.pkl"), extractor=_StubExtractor(), batch_size=4, decode_workers=3,
+                    decode="threads")
+    try:
+        a.create_feature_corpus(str(tmp_path / "imgs"))
+        b.create_feature_corpus(str(tmp_path / "imgs"))
+    finally:
+        a.close()
+    assert list(a.feature_dict) == list(b.feature_dict)
+    assert all(torch.equal(a.feature_dict[k], b.feature_dict[k]) for k in a.feature_dict)

@@ -238,3 +238,79 @@ def test_dp_nccl_world1_overlapped_allreduce():
     for name, (same_loss, same_grad, same_par, nb, diffs) in out.items():
         assert same_loss and same_grad and same_par, (name, same_loss, same_grad, same_par, diffs)
         assert len(nb) == 2 and sum(nb.values()) >= 2, (name, nb)  # buckets from both encoder streams
+
+
+def _worker_nccl_graph(port, q):
+    """world-1 RCCL: a DP trainer whose whole step (with the bucketed all-reduce) is captured in a
+    HIP graph vs the plain captured trainer, two replays on two batches each"""
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from mmfd.dp import GradAllReduce
+        from mmfd.train import FusionTrainer, build_flagship
+        from tests.smoke_impl import FULL, build_pair, tiny_batch
+        out = {}
+        t_dp, _ = build_pair("fp32", dropout=0.1, seed=5, with_oracle=False)
+        t_ref, _ = build_pair("fp32", dropout=0.1, seed=5, with_oracle=False)
+        dp = GradAllReduce(bucket_mb=0.05, force=True)
+        tr_dp = FusionTrainer(t_dp.text_encoder, t_dp.image_encoder, t_dp.head, lr=1e-3, precision="fp32", dp=dp)
+        tr_ref = FusionTrainer(t_ref.text_encoder, t_ref.image_encoder, t_ref.head, lr=1e-3, precision="fp32")
+        f_dp = build_flagship("cuda", "fp32", seed=42, dp=GradAllReduce(force=True))
+        f_ref = build_flagship("cuda", "fp32", seed=42)
+        for name, a, b, batches in (("tiny", tr_dp, tr_ref, [tiny_batch(4, seed=21), tiny_batch(4, seed=22),
+                                                             tiny_batch(4, seed=23)]),
+                                    ("full", f_dp, f_ref, [tiny_batch(1, cfg=FULL, seed=41),
+                                                           tiny_batch(1, cfg=FULL, seed=42),
+                                                           tiny_batch(1, cfg=FULL, seed=43)])):
+            static_a = {k: v.cuda() for k, v in batches[0].items()}
+            static_b = {k: v.cuda() for k, v in batches[0].items()}
+            a.capture(static_a, warmup=1)
+            b.capture(static_b, warmup=1)
+            names = [n for m in (a.text_encoder, a.image_encoder, a.head) for n, _ in m.named_parameters()]
+            emb = "embeddings.word_embeddings.weight"
+            ok = []
+            for bt in batches[1:]:
+                la = a.replay({k: v.cuda() for k, v in bt.items()}).clone()
+                lb = b.replay({k: v.cuda() for k, v in bt.items()}).clone()
+                torch.cuda.synchronize()
+                bad = []
+                for n, p, q_ in zip(names, a.params, b.params):
+                    tol = 1e-6 if n == emb else 0.0  # fp32 atomics in the word-embedding scatter-add
+                    for x, y in ((p.grad, q_.grad), (p.detach(), q_.detach())):
+                        if (x is None) != (y is None) or (x is not None and
+                                                          float((x - y).abs().max()) > tol * max(1.0, float(y.abs().max()))):
+                            bad.append(n)
+                ok.append((float((la - lb).abs().max()), bad[:8]))
+            out[name] = (ok, dict(a.dp.last_buckets))
+            a.release_graph()
+            b.release_graph()
+        q.put(out)
+    except BaseException:
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_nccl_world1_graph_captured_step():
+    """the data-parallel step captured as ONE HIP graph — forward, backward with the
+    per-stream bucket packs and the RCCL all_reduce kernels, finish()'s wait + unpack, AdamW — on
+    ProcessGroupNCCL (RCCL) with one rank. Replayed on new batches it must equal the plain captured
+    step (no DP) in losses, gradients and updated parameters, bit for bit (the word-embedding
+    gradient, accumulated with fp32 atomics, within 1e-6), tiny with 50 KB buckets and full size
+    with the default 32 MB buckets, dropout on."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_nccl_graph, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=500)
+    p.join(timeout=120)
+    assert "error" not in out, out.get("error")
+    assert p.exitcode == 0
+    for name, (steps, nb) in out.items():
+        for lerr, bad in steps:
+            assert lerr == 0.0 and not bad, (name, lerr, bad)
+        assert len(nb) == 2 and sum(nb.values()) >= 2, (name, nb)

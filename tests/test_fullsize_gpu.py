@@ -113,3 +113,106 @@ def test_config1_reference_default_head_matches_oracle(precision, factify):
         worst, nworst = max(worst, e), max(nworst, en)
     print(f"config1 factify={factify} {precision}: logits {yerr:.3e} loss {lerr:.3e} grad max-rel {worst:.3e} "
           f"norm-rel {nworst:.3e}")
+
+
+def _fixture(name):
+    import os
+
+    import numpy as np
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", name))
+
+
+def test_config3_bs256_step_matches_oracle():
+    """BASELINE config 3 at its OWN batch size: one fp32 full fine-tune step,
+    bs = 256 pairs (M = 65,536 text / 100,864 image token rows, the dW GEMMs' K over those rows, the
+    split-K cost model and the XCD tile order over full grids — the bench's launch geometry), dropout
+    0, against the oracle's chunked whole-batch gradient (tests/golden/make_config3_bs256.py:
+    oracle/train_step.chunked_loss_grads, train.py:146-170, stored as the loss vector plus per-tensor
+    max |g|, ||g|| and 512 strided gradient samples).
+      loss vector <= 1e-3 abs (north_star); per tensor: samples <= 2e-3 of max(|g| max, 1e-3 of the
+      largest gradient), max |g| and ||g|| within 2e-3 relative."""
+    import numpy as np
+
+    from tests.golden.make_config3_bs256 import B, BATCH_SEED, WEIGHT_SEED, sample_index
+    fx = _fixture("config3_bs256.npz")
+    torch.cuda.empty_cache()
+    tr, states = build_pair("fp32", dropout=0.0, cfg=FULL, seed=WEIGHT_SEED, lr=1e-4, with_oracle=False)
+    init = {}
+    for pre, sd in zip(("bert.", "vit.", "head."), states):
+        for k, v in sd.items():
+            init[pre + k] = v
+    names = [str(n) for n in fx["names"]]
+    for i, n in enumerate(names):  # the fixture was made from these exact initial weights
+        w = init[n].double()
+        assert abs(w.sum().item() - fx["init_sum"][i]) <= 1e-9 * max(1.0, fx["init_abs"][i]), f"stale fixture: {n}"
+    batch = tiny_batch(B, cfg=FULL, seed=BATCH_SEED)
+    dev = torch.device("cuda", 0)
+    loss = tr.step({k: v.to(dev) for k, v in batch.items()})
+    torch.cuda.synchronize()
+    lerr = np.abs(loss.double().cpu().numpy() - fx["loss"]).max()
+    assert lerr <= 1e-3, (loss.tolist(), fx["loss"].tolist())
+    from tests.smoke_impl import _named
+    mine = _named(tr)
+    assert set(names) <= set(mine), set(names) - set(mine)
+    floor = 1e-3 * float(fx["gmax"].max())
+    worst, wname, fails = 0.0, "", []
+    off = fx["offsets"]
+    for i, n in enumerate(names):
+        g = mine[n].grad
+        assert g is not None, n
+        gf = g.reshape(-1)
+        idx = torch.from_numpy(sample_index(gf.numel())).to(dev)
+        got = gf[idx].double().cpu().numpy()
+        want = fx["samples"][off[i]:off[i + 1]].astype(np.float64)
+        scale = max(float(fx["gmax"][i]), floor)
+        e = np.abs(got - want).max() / scale
+        em = abs(gf.abs().max().item() - fx["gmax"][i]) / scale
+        en = abs(gf.double().norm().item() - fx["gnorm"][i]) / max(float(fx["gnorm"][i]), 1e-30)
+        if max(e, em) > 2e-3 or (fx["gmax"][i] > floor and en > 2e-3):
+            fails.append(f"{n}: samples {e:.2e} max {em:.2e} norm {en:.2e}")
+        if e > worst:
+            worst, wname = e, n
+    print(f"config3 bs=256 fp32: loss err {lerr:.3e}, worst sampled grad err {worst:.3e} ({wname}), "
+          f"{len(names)} tensors")
+    assert not fails, "; ".join(fails[:8])
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_config2_bs64_forward_logits_match_oracle():
+    """BASELINE config 2 at its OWN batch size: bert-base-uncased + ViT-B/16 +
+    the fusion head, forward only in eval mode, bs = 64 pairs with ragged text masks, fp32, through
+    FusionTrainer.predict (the bench's forward workload) — all four paths' logits within 1e-3 of the
+    oracle (oracle.encoders + oracle.fusion_head, evaluate.py:112-164 batched)."""
+    from oracle import encoders as OE
+    from tests.smoke_impl import oracle_cfgs
+    torch.cuda.empty_cache()
+    Bp = 64
+    tr, states = build_pair("fp32", dropout=0.1, cfg=FULL, seed=9, with_oracle=False)
+    batch = tiny_batch(Bp, cfg=FULL, seed=64)
+    dev = torch.device("cuda", 0)
+    out = tr.predict({k: v.to(dev) for k, v in batch.items()})
+    torch.cuda.synchronize()
+    bcfg, vcfg = oracle_cfgs(FULL)
+    bp, vp, hp = states
+    ys = [y.detach().double().cpu() for pr in out for y in pr]
+    with torch.no_grad():
+        refs = []
+        for s in range(0, Bp, 16):  # chunks bound the CPU memory; eval mode has no batch coupling
+            e = s + 16
+            ids = torch.cat([batch["input_ids"][s:e], batch["input_ids"][Bp + s:Bp + e]])
+            mask = torch.cat([batch["attention_mask"][s:e], batch["attention_mask"][Bp + s:Bp + e]])
+            px = torch.cat([batch["pixel_values"][s:e], batch["pixel_values"][Bp + s:Bp + e]])
+            T = OE.bert_forward(bp, ids, mask, None, num_layers=bcfg["num_hidden_layers"],
+                                num_heads=bcfg["num_attention_heads"])
+            I = OE.vit_forward(vp, px, num_layers=vcfg["num_hidden_layers"], num_heads=vcfg["num_attention_heads"],
+                               patch=vcfg["patch_size"])
+            r = OF.model_forward(hp, T[:16], I[:16], T[16:], I[16:], num_heads=FULL["head_heads"])
+            refs.append([y for pr in r for y in pr])
+    ref = [torch.cat([c[j] for c in refs]).double() for j in range(4)]
+    errs = [(y - r).abs().max().item() for y, r in zip(ys, ref)]
+    print(f"config2 bs=64 fp32 logits err per path {['%.2e' % e for e in errs]}, |logit| max "
+          f"{max(r.abs().max().item() for r in ref):.2f}")
+    assert max(errs) <= 1e-3, errs
+    del tr
+    torch.cuda.empty_cache()

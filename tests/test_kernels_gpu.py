@@ -526,6 +526,44 @@ def test_gemm_fp32_split_operands_error_matches_fp32_mfma(layout, shape):
     assert err["split"] <= 1e-5 * math.sqrt(Kd / 768), err
 
 
+@pytest.mark.parametrize("layout,shape", [
+    ("nn", (65536, 2304, 768)),    # BERT QKV forward at bs = 256 (512 sequences x 128 tokens)
+    ("nn", (100864, 3072, 768)),   # ViT FFN1 forward (512 images x 197 tokens)
+    ("nn", (100864, 768, 3072)),   # ViT FFN2 forward
+    ("nt", (65536, 768, 3072)),    # BERT FFN1 dX (dPre [tokens, 3072] x W1)
+    ("nt", (100864, 3072, 768)),   # ViT FFN2 dX (dY [tokens, 768] x W2)
+    ("tt", (3072, 768, 100864)),   # ViT FFN1 dW: K over every image token row (split-K)
+    ("tt", (2304, 768, 65536)),    # BERT QKV dW
+    ("tt", (768, 3072, 65536))])   # BERT FFN2 dW
+def test_gemm_fp32_split_operands_bench_shapes(layout, shape):
+    """The split-operand fp32 GEMM at the bs = 256 step's own launch shapes (the
+    full grids' XCD tile order, the split-K cost model at K = 65,536 / 100,864): error against an
+    fp64 product within 1.5x of the fp32 MFMA's own (+1e-7 of the output scale), as
+    test_gemm_fp32_split_operands_error_matches_fp32_mfma. Operands are drawn on the device."""
+    M, N, Kd = shape
+    ta, tb = layout[0] == "t", layout[1] == "t"
+    assert K.x6_ok(M, N, Kd, ta, tb)
+    g = torch.Generator(DEV).manual_seed(M + N + Kd)
+    A = torch.randn((Kd, M) if ta else (M, Kd), generator=g, device=DEV)
+    B = torch.randn((Kd, N) if tb else (N, Kd), generator=g, device=DEV) * 0.05
+    ref = (A.double().T if ta else A.double()) @ (B.double() if tb else B.double().T)
+    outs = {}
+    old = K.set_fp32_gemm_mode("split")
+    try:
+        for mode in ("split", "native"):
+            K.set_fp32_gemm_mode(mode)
+            outs[mode] = K.gemm(A, B, trans_a=ta, trans_b=tb)
+        torch.cuda.synchronize()
+    finally:
+        K.set_fp32_gemm_mode(old)
+    scale = ref.abs().max().item()
+    err = {m: (o.double() - ref).abs().max().item() / scale for m, o in outs.items()}
+    print(f"{layout} {shape}: split {err['split']:.3e} native {err['native']:.3e}")
+    assert err["split"] <= 1.5 * err["native"] + 1e-7, err
+    del A, B, ref, outs
+    torch.cuda.empty_cache()
+
+
 def test_gemm_fp32_split_operands_epilogues_rowsum():
     """the split path keeps the fp32 epilogues (bias, GELU + saved pre-activation, residual, dropout,
     beta) and the fused bias-gradient row sums of op(A), with and without split-K"""

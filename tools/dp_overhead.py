@@ -3,7 +3,8 @@
   eager  — eager steps, two encoder streams, no DP,
   dp     — eager steps with the overlapped gradient all-reduce active on RCCL (ProcessGroupNCCL with
            one rank, mmfd.dp.GradAllReduce(force=True), default 32 MB per-stream buckets: packing,
-           all_reduce calls, finish() wait + unpack — everything a rank does except the xGMI transfer).
+           all_reduce calls, finish() wait + unpack — everything a rank does except the xGMI transfer),
+  dp_graph — the same DP step captured as one HIP graph (the N > 1 bench path since round 4).
   python tools/dp_overhead.py [steps]"""
 import os
 import socket
@@ -51,7 +52,12 @@ torch.cuda.empty_cache()
 dp = GradAllReduce(force=True)
 tr = build_flagship(dev, "fp32", seed=42, dp=dp)
 res["dp"] = timed(lambda: tr.step(batch), steps)
-print({k: round(v, 1) for k, v in res.items()}, "buckets per stream:", dp.last_buckets, flush=True)
+nb = dict(dp.last_buckets)
+tr.capture(batch, warmup=1)
+res["dp_graph"] = timed(tr.replay, steps)
+tr.release_graph()
+print({k: round(v, 1) for k, v in res.items()}, "buckets per stream:", nb, flush=True)
 print(f"DP bookkeeping + RCCL calls: {res['dp'] - res['eager']:+.1f} ms/step over eager; eager over graph: "
-      f"{res['eager'] - res['graph']:+.1f} ms/step", flush=True)
+      f"{res['eager'] - res['graph']:+.1f} ms/step; captured DP step over graph: "
+      f"{res['dp_graph'] - res['graph']:+.1f} ms/step ({100 * (res['dp_graph'] / res['graph'] - 1):+.2f} %)", flush=True)
 dist.destroy_process_group()
