@@ -35,6 +35,9 @@ constexpr uint32_t X6_RS = 0x25;   // segments whose A plane appears once (m, l,
 // operand layout of `a` (A / B = the bf16 planes pa / pb, x6.nkt = 32-deep K-steps in all)
 void dispatch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
                   int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
+// the same product on four waves with AGPR accumulators (gemm_x6w.hip, gemm256_x6w_kernel)
+void dispatch_x6w(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
+                  int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
 }  // namespace mmfd_gemmx
 
 namespace {
@@ -44,6 +47,7 @@ using mmfd_gemmx::X6_CA;
 using mmfd_gemmx::X6_CB;
 using mmfd_gemmx::X6_RS;
 using mmfd_gemmx::dispatch_x6f;
+using mmfd_gemmx::dispatch_x6w;
 
 
 // Tile geometry: 256 (M) x 128 (N) x 128 B of K (64 bf16 / 32 fp32), 8 waves as 4 (M) x 2 (N), each
@@ -474,6 +478,68 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 #else
 #define G8_STAMP(k) do { } while (0)
 #endif
+
+// Split-operand LDS slots (gemm_x6f.hip, gemm_x6w.hip): one plane of one 128-row / 128-column half-tile of a
+// 32-deep K-step, 8 KB
+constexpr int XF_SLOT = 8192;
+constexpr int XF_BK = 32;  // K per step
+
+template <int LAYOUT> struct XfImg;  // LDS slot image of one plane of one half-tile
+template <> struct XfImg<0> {        // [128 rows][64 B]
+  static constexpr int CPR = 4, RPI = 16;  // 64-B rows
+  __device__ __forceinline__ static int swz(int r, int c) { return c ^ ((r >> 2) & 2); }
+};
+template <> struct XfImg<1> {  // [32 K rows][128 bf16]
+  static constexpr int CPR = 16, RPI = 4;  // 256-B rows
+  __device__ __forceinline__ static int swz(int r, int c) { return Img<bf16, 1, 128>::swz(r, c); }
+};
+
+// one 1-KB piece of one plane slot per wave (8 waves fill the 8-KB slot)
+template <int LAYOUT>
+struct XfFill {
+  uint32_t off;
+  int cbase;  // layout 0: the element column (k) of this lane's chunk within the K-step
+  __device__ __forceinline__ void init(int64_t ld, int64_t mn0, int64_t mn_ext, int wave, int lane) {
+    using I = XfImg<LAYOUT>;
+    const int row = wave * I::RPI + lane / I::CPR;
+    const int c = I::swz(row, lane % I::CPR);
+    int64_t el;
+    bool ok;
+    if (LAYOUT == 0) { el = (mn0 + row) * ld + (int64_t)c * 8; ok = mn0 + row < mn_ext; cbase = c * 8; }
+    else { el = (int64_t)row * ld + mn0 + (int64_t)c * 8; ok = mn0 + (int64_t)c * 8 < mn_ext; cbase = 0; }
+    off = ok ? (uint32_t)(el * 2) : OOB;
+  }
+  // soff: byte offset of (plane, K-step) in the operand's planes
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* slot, uint32_t soff, int64_t k0, int64_t K,
+                                        int wave) const {
+    uint32_t o = off;
+    if (LAYOUT == 0 && k0 + XF_BK > K && k0 + (int64_t)cbase >= K) o = OOB;  // partial last K-step
+    dma16(rs, slot + wave * 1024, o, soff);
+  }
+};
+
+// fragment of 16 rows (A) of a layout-0 slot: lane (g, i) = row sub*16 + i, k-chunk g
+__device__ __forceinline__ uint4 xf_frag_a0(const char* img, int sub, int lane) {
+  const int g = lane >> 4, i = lane & 15, row = sub * 16 + i;
+  return lds_read16(img, row * 64 + (XfImg<0>::swz(row, g) << 4));
+}
+template <int LAYOUT>
+__device__ __forceinline__ uint4 xf_frag_a(const char* img, int sub, int lane) {
+  if constexpr (LAYOUT == 0) return xf_frag_a0(img, sub, lane);
+  else return load_frag<bf16, 1, 128>(img, sub, 0, lane);
+}
+// B fragment j of the wave's 32 columns (column units 2p + j, see g8_load_b)
+template <int LAYOUT>
+__device__ __forceinline__ uint4 xf_frag_b(const char* img, int wc, int j, int lane) {
+  if constexpr (LAYOUT == 0) {
+    const int g = lane >> 4, i = lane & 15;
+    const int row = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
+    return lds_read16(img, row * 64 + (XfImg<0>::swz(row, g) << 4));
+  } else {
+    return g8_load_b<bf16, 1>(img, wc, j, 0, lane);
+  }
+}
+
 
 // Epilogue of the 256x256 kernels (gemm256_kernel, gemm256_x6f_kernel): two passes of 128 rows
 // (quadrant row mq = pass); every wave stages its fp32 accumulators, then all threads apply the

@@ -60,65 +60,6 @@ __device__ uint64_t xf_stamps[4096 * 8 * 20];
 #define XF_TSTAMP(k) do { } while (0)
 #endif
 
-constexpr int XF_SLOT = 8192;
-constexpr int XF_BK = 32;  // K per step
-
-template <int LAYOUT> struct XfImg;  // LDS slot image of one plane of one half-tile
-template <> struct XfImg<0> {        // [128 rows][64 B]
-  static constexpr int CPR = 4, RPI = 16;  // 64-B rows
-  __device__ __forceinline__ static int swz(int r, int c) { return c ^ ((r >> 2) & 2); }
-};
-template <> struct XfImg<1> {  // [32 K rows][128 bf16]
-  static constexpr int CPR = 16, RPI = 4;  // 256-B rows
-  __device__ __forceinline__ static int swz(int r, int c) { return Img<bf16, 1, 128>::swz(r, c); }
-};
-
-// one 1-KB piece of one plane slot per wave (8 waves fill the 8-KB slot)
-template <int LAYOUT>
-struct XfFill {
-  uint32_t off;
-  int cbase;  // layout 0: the element column (k) of this lane's chunk within the K-step
-  __device__ __forceinline__ void init(int64_t ld, int64_t mn0, int64_t mn_ext, int wave, int lane) {
-    using I = XfImg<LAYOUT>;
-    const int row = wave * I::RPI + lane / I::CPR;
-    const int c = I::swz(row, lane % I::CPR);
-    int64_t el;
-    bool ok;
-    if (LAYOUT == 0) { el = (mn0 + row) * ld + (int64_t)c * 8; ok = mn0 + row < mn_ext; cbase = c * 8; }
-    else { el = (int64_t)row * ld + mn0 + (int64_t)c * 8; ok = mn0 + (int64_t)c * 8 < mn_ext; cbase = 0; }
-    off = ok ? (uint32_t)(el * 2) : OOB;
-  }
-  // soff: byte offset of (plane, K-step) in the operand's planes
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* slot, uint32_t soff, int64_t k0, int64_t K,
-                                        int wave) const {
-    uint32_t o = off;
-    if (LAYOUT == 0 && k0 + XF_BK > K && k0 + (int64_t)cbase >= K) o = OOB;  // partial last K-step
-    dma16(rs, slot + wave * 1024, o, soff);
-  }
-};
-
-// fragment of 16 rows (A) of a layout-0 slot: lane (g, i) = row sub*16 + i, k-chunk g
-__device__ __forceinline__ uint4 xf_frag_a0(const char* img, int sub, int lane) {
-  const int g = lane >> 4, i = lane & 15, row = sub * 16 + i;
-  return lds_read16(img, row * 64 + (XfImg<0>::swz(row, g) << 4));
-}
-template <int LAYOUT>
-__device__ __forceinline__ uint4 xf_frag_a(const char* img, int sub, int lane) {
-  if constexpr (LAYOUT == 0) return xf_frag_a0(img, sub, lane);
-  else return load_frag<bf16, 1, 128>(img, sub, 0, lane);
-}
-// B fragment j of the wave's 32 columns (column units 2p + j, see g8_load_b)
-template <int LAYOUT>
-__device__ __forceinline__ uint4 xf_frag_b(const char* img, int wc, int j, int lane) {
-  if constexpr (LAYOUT == 0) {
-    const int g = lane >> 4, i = lane & 15;
-    const int row = wc * 32 + 4 * (2 * (i >> 2) + j) + (i & 3);
-    return lds_read16(img, row * 64 + (XfImg<0>::swz(row, g) << 4));
-  } else {
-    return g8_load_b<bf16, 1>(img, wc, j, 0, lane);
-  }
-}
-
 // the six plane products of one K-step for one quadrant: per (i, j) a chain from zero, then one
 // fp32 add into the accumulator (a[i][p] / b[j][p]: plane p = hi, mid, lo). The two chains of an A
 // subtile run interleaved, and their adds are placed after the next subtile's first products (the

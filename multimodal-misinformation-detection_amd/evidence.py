@@ -289,6 +289,14 @@ class ImageSimilarity:
             self._pre = ImagePreprocessor("retrieval", device=self.device)
         return self._pre(images)
 
+    def preprocess_device(self, src, shapes, offsets):
+        """decoded uint8 HWC pixels already in the device buffer `src` -> normalised fp32 [N, 3, 224,
+        224] (the "retrieval" transform; see ImagePreprocessor.from_device)"""
+        if self._pre is None:
+            from .preprocess import ImagePreprocessor
+            self._pre = ImagePreprocessor("retrieval", device=self.device)
+        return self._pre.from_device(src, shapes, offsets)
+
     def extract_batch(self, pixels):
         """normalised fp32 [N, 3, 224, 224] (host or device) -> fp32 [N, 2048] on the device"""
         return self.model(pixels).flatten(1)
@@ -368,12 +376,40 @@ class ImageCorpus:
         if self._pool is not None:
             self._pool.close()
             self._pool = None
+        if getattr(self, "_ring", None) is not None:
+            self._ring.close()
+            self._ring = None
+
+    def _decode_ring(self):
+        ring = getattr(self, "_ring", None)
+        if ring is None or ring.gps * ring.group < self.batch_size:
+            from .hostdecode import PinnedDecodeRing
+            if ring is not None:
+                ring.close()
+            ring = self._ring = PinnedDecodeRing(self.batch_size, self.feature_extractor.device, self.decode_workers)
+        return ring
 
     def _extract_paths(self, paths):
         out = {}
         chunks = [paths[i:i + self.batch_size] for i in range(0, len(paths), self.batch_size)]
         if not chunks:
             return out
+        ex = self.feature_extractor
+        if (self.decode == "processes" and self.decode_workers > 1 and hasattr(ex, "preprocess_device")
+                and torch.device(ex.device).type == "cuda"):
+            # the workers decode into a page-locked shared ring, the batch's pixels go to the device
+            # with asynchronous copies, and the features stay on the device until the build is done:
+            # the host thread only submits and enqueues, so decode, upload and the GPU overlap
+            ring = self._decode_ring()
+            h = ring.submit(chunks[0], 0)
+            feats = []
+            for ci, chunk in enumerate(chunks):
+                src, shapes, offs = ring.upload(h, ci % 2)
+                if ci + 1 < len(chunks):
+                    h = ring.submit(chunks[ci + 1], (ci + 1) % 2)
+                feats.append(ex.extract_batch(ex.preprocess_device(src, shapes, offs)).float())
+            allf = torch.cat(feats).cpu()
+            return {p: allf[i].clone() for i, p in enumerate(paths)}
         if self.decode == "processes" and self.decode_workers > 1:
             pool = self._decode_pool()
             nxt = pool.submit(chunks[0])

@@ -90,3 +90,130 @@ class DecodePool:
             self._ex.shutdown(wait=False, cancel_futures=True)
         except Exception:
             pass
+
+
+# ---- decode straight into page-locked shared memory (no host copies in the caller) -------------------
+_ATTACHED = {}
+
+
+def _decode_group_into(shm_name, base, cap, paths):
+    """worker: decode `paths` into the shared ring at [base, base + cap), packed back to back ->
+    [(h, w, offset from base)] with offset -1 and the pixels themselves for an image past the space"""
+    from PIL import Image
+    shm = _ATTACHED.get(shm_name)
+    if shm is None:
+        shm = _ATTACHED[shm_name] = shared_memory.SharedMemory(name=shm_name)
+        resource_tracker.unregister(shm._name, "shared_memory")
+    out, off = [], 0
+    for p in paths:
+        with Image.open(p) as im:
+            a = np.asarray(im.convert("RGB"), dtype=np.uint8)
+        if off + a.nbytes <= cap:
+            np.frombuffer(shm.buf, dtype=np.uint8, count=a.nbytes, offset=base + off)[:] = a.reshape(-1)
+            out.append((a.shape[0], a.shape[1], off, None))
+            off += a.nbytes
+        else:
+            out.append((a.shape[0], a.shape[1], -1, a))
+    return out
+
+
+class PinnedDecodeRing:
+    """Host decode for the GPU corpus build without host-side copies: a POSIX shared-memory ring,
+    page-locked for the HIP runtime once (hipHostRegister through torch's cudart binding), that the
+    decode worker processes write into directly. `submit(paths, slot)` starts decoding one batch into
+    ring slot `slot` (groups of `group` images, `cap` bytes per image on average per group, packed);
+    `upload(handle, slot)` issues the asynchronous host->device copies of the batch's pixels and
+    returns (device uint8 buffer, [(h, w)], [byte offsets]); the slot is reused only after the
+    stream has consumed its copies (an event per slot). Images that do not fit their group's space
+    come back through the pipe and are uploaded from ordinary memory."""
+
+    def __init__(self, batch, device, workers=None, group=8, cap=1 << 20, slots=2):
+        import concurrent.futures as cf
+        import ctypes
+        import multiprocessing as mp
+
+        import torch
+        self.device = torch.device(device)
+        self.workers = int(workers or min(16, len(os.sched_getaffinity(0))))
+        self.group, self.slots = max(1, int(group)), int(slots)
+        self.gbytes = self.group * int(cap)
+        self.gps = (int(batch) + self.group - 1) // self.group
+        self.sbytes = self.gps * self.gbytes
+        self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self.sbytes)
+        self._addr = ctypes.addressof(ctypes.c_char.from_buffer(self.shm.buf))
+        rc = torch._C._cudart.cudaHostRegister(self._addr, self.slots * self.sbytes, 0)
+        if int(rc) != 0:
+            self.shm.close()
+            self.shm.unlink()
+            raise RuntimeError(f"hipHostRegister of the decode ring failed ({rc})")
+        self.host = torch.frombuffer(self.shm.buf, dtype=torch.uint8)
+        self._events = [None] * self.slots
+        ctx = mp.get_context("forkserver")
+        ctx.set_forkserver_preload([__name__, "PIL.Image"])
+        self._ex = cf.ProcessPoolExecutor(max_workers=self.workers, mp_context=ctx)
+
+    def submit(self, paths, slot):
+        ev = self._events[slot]
+        if ev is not None:
+            ev.synchronize()  # the previous batch's copies out of this slot have run
+            self._events[slot] = None
+        paths = list(paths)
+        if len(paths) > self.gps * self.group:
+            raise ValueError("batch larger than the ring slot")
+        return [self._ex.submit(_decode_group_into, self.shm.name, slot * self.sbytes + gi * self.gbytes, self.gbytes,
+                                paths[i:i + self.group])
+                for gi, i in enumerate(range(0, len(paths), self.group))]
+
+    def upload(self, handle, slot):
+        import torch
+        res = [f.result() for f in handle]
+        shapes, offs, spans, extra, total = [], [], [], [], 0
+        for gi, items in enumerate(res):
+            used = 0
+            for h, w, off, arr in items:
+                shapes.append((h, w))
+                if off >= 0:
+                    offs.append(None)  # filled below: the group's bytes land contiguously
+                    used = max(used, off + h * w * 3)
+                else:
+                    offs.append(None)
+                    extra.append((len(shapes) - 1, arr))
+            spans.append((gi, used))
+        dsrc = torch.empty(max(1, sum(u for _, u in spans) + sum(a.nbytes for _, a in extra)), dtype=torch.uint8,
+                           device=self.device)
+        k, pos = 0, 0
+        for (gi, used), items in zip(spans, res):
+            base = slot * self.sbytes + gi * self.gbytes
+            if used:
+                dsrc[pos:pos + used].copy_(self.host[base:base + used], non_blocking=True)
+            for h, w, off, arr in items:
+                if off >= 0:
+                    offs[k] = pos + off
+                k += 1
+            pos += used
+        for i, arr in extra:
+            dsrc[pos:pos + arr.nbytes].copy_(torch.from_numpy(arr.reshape(-1)))
+            offs[i] = pos
+            pos += arr.nbytes
+        ev = torch.cuda.Event()
+        ev.record()
+        self._events[slot] = ev
+        return dsrc, shapes, offs
+
+    def close(self):
+        import torch
+        if self._ex is None:
+            return
+        self._ex.shutdown(wait=True, cancel_futures=True)
+        self._ex = None
+        torch.cuda.synchronize(self.device)
+        torch._C._cudart.cudaHostUnregister(self._addr)
+        del self.host
+        self.shm.close()
+        self.shm.unlink()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

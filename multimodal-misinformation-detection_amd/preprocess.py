@@ -154,6 +154,18 @@ class ImagePreprocessor:
                                                 self._std, K._ptr(out), K._stream()), "mmfd_resize_normalize")
         return out
 
+    def from_device(self, src, shapes, offsets):
+        """The batch whose uint8 HWC pixels already sit in the device buffer `src` (image i at byte
+        offsets[i], shape shapes[i] = (h, w)) -> fp32 [N, 3, S, S]: no host staging at all
+        (mmfd.hostdecode.PinnedDecodeRing uploads the decoded pixels there asynchronously)."""
+        Ho, Wo = self.out_hw
+        if not shapes:
+            return torch.empty(0, 3, Ho, Wo, device=self.device, dtype=torch.float32)
+        plan = self.plan(list(shapes), [src.data_ptr() + int(o) for o in offsets])
+        out = self.launch(plan)
+        out._keepalive = (src, plan)  # until the stream has consumed them
+        return out
+
     def __call__(self, images):
         arrs = [_as_uint8_rgb(im) for im in images]
         n = len(arrs)

@@ -141,6 +141,37 @@ def test_image_similarity_and_corpus(tmp_path):
     assert (fb[0] - f).abs().max().item() < 1e-4
 
 
+def test_corpus_pinned_ring_equals_thread_decode(tmp_path):
+    """config 5 host path: the corpus build that decodes in worker processes
+    straight into the page-locked shared ring (mmfd.hostdecode.PinnedDecodeRing: asynchronous
+    uploads, device-side preprocessing from the uploaded pixels, features kept on the device until
+    the end) gives bit-identical features to the round-3 thread-pool decode + host staging; a ring
+    with a small per-image space sends the larger images through the overflow path."""
+    from PIL import Image
+
+    from mmfd.hostdecode import PinnedDecodeRing
+    rng = np.random.default_rng(3)
+    d = tmp_path / "imgs"
+    d.mkdir()
+    for i in range(23):  # mixed sizes and formats, three batches of 8 (the last ragged)
+        h, w = 60 + 13 * (i % 7), 80 + 11 * (i % 5)
+        im = Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8))
+        im.save(d / f"x{i:02d}.{'png' if i % 3 == 0 else 'jpg'}")
+    ext = ImageSimilarity(model=ResNet((1, 1, 1, 1), 8), precision="fp32")
+    thr = ImageCorpus(str(tmp_path / "t.pkl"), extractor=ext, batch_size=8, decode_workers=3, decode="threads")
+    thr.create_feature_corpus(str(d))
+    for cap in (1 << 20, 4 * 4096):  # roomy / most images overflow their group's space
+        ring = ImageCorpus(str(tmp_path / f"r{cap}.pkl"), extractor=ext, batch_size=8, decode_workers=3)
+        ring._ring = PinnedDecodeRing(8, DEV, workers=3, group=3, cap=cap)
+        try:
+            ring.create_feature_corpus(str(d))
+        finally:
+            ring.close()
+        assert list(ring.feature_dict) == list(thr.feature_dict)
+        for k in thr.feature_dict:
+            assert torch.equal(ring.feature_dict[k], thr.feature_dict[k]), (cap, k)
+
+
 # ---- MPNet (a13) ------------------------------------------------------------------------------------
 def _mpnet_from_fixture(z, precision):
     cfg = json.loads(str(z["config"]))

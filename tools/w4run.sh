@@ -1,0 +1,10 @@
+set -e
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+rm -f gpurun_out/r04_w4stamps.log
+timeout -k 10 240 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "x6w" > gpurun_out/r04_x6w_test.log 2>&1 || { echo X6W_TEST_FAILED; tail -30 gpurun_out/r04_x6w_test.log; exit 1; }
+echo X6W_TEST_OK
+timeout -k 10 300 python tools/x6w_ab.py 3 > gpurun_out/r04_x6w_ab.log 2>&1 || { echo X6W_AB_FAILED; tail -20 gpurun_out/r04_x6w_ab.log; exit 1; }
+for v in "" d2 d3; do
+  W4_VARIANT=$v timeout -k 10 120 python tools/w4_stamps.py 100864 3072 768 fwd >> gpurun_out/r04_w4stamps.log 2>&1
+done
