@@ -504,12 +504,6 @@ bool x6_fused() {
   static const bool seg = getenv("MMFD_X6_SEGMENTED") != nullptr;
   return !seg;
 }
-// fused-plane kernel: 1 = four waves with AGPR accumulators (gemm256_x6w_kernel), 0 = eight waves in
-// two ping-pong rows (gemm256_x6f_kernel); identical results (env MMFD_X6W, mmfd_debug_set_x6w)
-int g_x6w = [] {
-  const char* v = getenv("MMFD_X6W");
-  return v ? (atoi(v) != 0 ? 1 : 0) : 0;
-}();
 
 // fp32 operand -> three bf16 planes (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid),
 // each difference exact in fp32): stored rows x cols (ld) -> planes [3][rows][cols]; 8 columns per
@@ -715,13 +709,6 @@ extern "C" int mmfd_set_fp32_gemm_mode(int mode) {
   return old;
 }
 
-// A/B switch between the two fused-plane kernels (not part of include/mmfd.h): returns the old value
-extern "C" int mmfd_debug_set_x6w(int on) {
-  const int old = g_x6w;
-  g_x6w = on ? 1 : 0;
-  return old;
-}
-
 extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   MMFD_CHECK_ARG(ap != nullptr, "mmfd_gemm: null args");
   const mmfd_gemm_args& a = *ap;
@@ -836,9 +823,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     }
     MMFD_CHECK_LAUNCH("split3");
     if (xf) {
-      const X6Args x6{nkt, (uint32_t)xp.pa, (uint32_t)xp.pb};
-      if (g_x6w) dispatch_x6w(a, e, ws, splits, tps, rs_out, rs_mode, s, pa, pb, x6);
-      else dispatch_x6f(a, e, ws, splits, tps, rs_out, rs_mode, s, pa, pb, x6);
+      dispatch_x6f(a, e, ws, splits, tps, rs_out, rs_mode, s, pa, pb, X6Args{nkt, (uint32_t)xp.pa, (uint32_t)xp.pb});
     } else {
       const X6Args x6{(int)((a.K + 63) / 64), (uint32_t)xp.pa, (uint32_t)xp.pb};
       dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s, &x6, pa, pb);

@@ -35,9 +35,6 @@ constexpr uint32_t X6_RS = 0x25;   // segments whose A plane appears once (m, l,
 // operand layout of `a` (A / B = the bf16 planes pa / pb, x6.nkt = 32-deep K-steps in all)
 void dispatch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
                   int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
-// the same product on four waves with AGPR accumulators (gemm_x6w.hip, gemm256_x6w_kernel)
-void dispatch_x6w(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
-                  int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
 }  // namespace mmfd_gemmx
 
 namespace {
@@ -47,7 +44,6 @@ using mmfd_gemmx::X6_CA;
 using mmfd_gemmx::X6_CB;
 using mmfd_gemmx::X6_RS;
 using mmfd_gemmx::dispatch_x6f;
-using mmfd_gemmx::dispatch_x6w;
 
 
 // Tile geometry: 256 (M) x 128 (N) x 128 B of K (64 bf16 / 32 fp32), 8 waves as 4 (M) x 2 (N), each
@@ -479,7 +475,7 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 #define G8_STAMP(k) do { } while (0)
 #endif
 
-// Split-operand LDS slots (gemm_x6f.hip, gemm_x6w.hip): one plane of one 128-row / 128-column half-tile of a
+// Split-operand LDS slots (gemm_x6f.hip): one plane of one 128-row / 128-column half-tile of a
 // 32-deep K-step, 8 KB
 constexpr int XF_SLOT = 8192;
 constexpr int XF_BK = 32;  // K per step

@@ -147,8 +147,18 @@ def test_config3_bs256_step_matches_oracle():
         assert abs(w.sum().item() - fx["init_sum"][i]) <= 1e-9 * max(1.0, fx["init_abs"][i]), f"stale fixture: {n}"
     batch = tiny_batch(B, cfg=FULL, seed=BATCH_SEED)
     dev = torch.device("cuda", 0)
-    loss = tr.step({k: v.to(dev) for k, v in batch.items()})
+    db = {k: v.to(dev) for k, v in batch.items()}
     torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
+    loss = tr.step(db)
+    torch.cuda.synchronize()
+    # device-memory bound of the eager bs = 256 step (profiles/r04_memory.json:
+    # 166.3 GiB peak with 2.5 GiB resident, of which 161.1 GiB are what the forward saves for the
+    # backward — 45.9 GiB of it split-operand activation planes, 1.0 GiB weight planes)
+    step_gib = (torch.cuda.max_memory_allocated(dev) - base) / 2**30
+    print(f"config3 bs=256 eager step: {step_gib:.1f} GiB above the {base / 2**30:.1f} GiB before it")
+    assert step_gib <= 175.0, step_gib
     lerr = np.abs(loss.double().cpu().numpy() - fx["loss"]).max()
     assert lerr <= 1e-3, (loss.tolist(), fx["loss"].tolist())
     from tests.smoke_impl import _named

@@ -763,54 +763,3 @@ def test_gemm_single_tile_weight_gradient_many_splits(dtype):
     tol = (1e-5 if dtype == torch.float32 else 2e-3) * ref.abs().max().item()
     assert (dw.double() - ref).abs().max().item() <= tol
     assert (rs.double() - (0.25 + dy.double().sum(0))).abs().max().item() <= 1e-4 * math.sqrt(Kd)
-
-
-@pytest.mark.parametrize("layout", ["nn", "nt", "tn", "tt"])
-@pytest.mark.parametrize("shape", [(512, 768, 768), (1000, 520, 200), (300, 264, 1056), (768, 256, 4096),
-                                   (256, 2304, 65536), (4096, 3072, 768)])
-def test_gemm_x6w_four_wave_kernel_bitwise_equals_x6f(layout, shape):
-    """The four-wave AGPR split-operand kernel (gemm256_x6w_kernel) runs the same six plane products
-    per 32-deep K-step in the same order per accumulator element as the eight-wave ping-pong kernel
-    (gemm256_x6f_kernel): C, the fused bias-gradient row sums and the output planes must be
-    bit-identical, with bias + GELU + saved pre-activation, with residual, and through split-K (the
-    K = 65,536 weight-gradient shape), over ragged M / N tiles and every operand layout."""
-    import ctypes
-    lib = K.lib()
-    lib.mmfd_debug_set_x6w.argtypes = [ctypes.c_int]
-    lib.mmfd_debug_set_x6w.restype = ctypes.c_int
-    M, N, Kd = shape
-    ta, tb = layout[0] == "t", layout[1] == "t"
-    old_mode = K.set_fp32_gemm_mode("split")
-    try:
-        if not K.x6_ok(M, N, Kd, ta, tb):
-            pytest.skip("MN-contiguous operands need whole 32-row K-steps on the split path")
-        g = torch.Generator(DEV).manual_seed(M * 7 + N + Kd)
-        A = torch.randn((Kd, M) if ta else (M, Kd), generator=g, device=DEV)
-        B = torch.randn((Kd, N) if tb else (N, Kd), generator=g, device=DEV) * 0.05
-        bias = torch.randn(N, generator=g, device=DEV)
-        res = torch.randn(M, N, generator=g, device=DEV)
-        cases = [dict(), dict(bias=bias, act=K.ACT_GELU, aux="aux"), dict(residual=res, bias=bias),
-                 dict(a_rowsum="rs")]
-        outs = {}
-        for w in (0, 1):
-            old = lib.mmfd_debug_set_x6w(w)
-            try:
-                got = []
-                for c in cases:
-                    kw = dict(c)
-                    if kw.get("aux") == "aux":
-                        kw["aux"] = torch.empty(M, N, device=DEV)
-                    if kw.get("a_rowsum") == "rs":
-                        kw["a_rowsum"] = torch.empty(M, device=DEV)
-                    pl = torch.empty(3, M, N, device=DEV, dtype=torch.bfloat16) if N % 8 == 0 else None
-                    y = K.gemm(A, B, trans_a=ta, trans_b=tb, out_planes=pl, **kw)
-                    got.append([y] + [kw[k] for k in ("aux", "a_rowsum") if k in kw] + ([pl] if pl is not None else []))
-                torch.cuda.synchronize()
-                outs[w] = got
-            finally:
-                lib.mmfd_debug_set_x6w(old)
-        for ci, (a, b) in enumerate(zip(outs[0], outs[1])):
-            for x, y in zip(a, b):
-                assert torch.equal(x, y), (ci, (x.float() - y.float()).abs().max().item())
-    finally:
-        K.set_fp32_gemm_mode(old_mode)
