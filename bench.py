@@ -835,11 +835,12 @@ def main():
                                    "(SURVEY 8(d), algorithmic)"},
             "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
             "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"],
-            "peak_memory_gb": res["peak_memory_gb"],
-            "fp32_gemm": ("split operands: x = hi + mid + lo bf16 planes staged together per 32-deep K-step, six bf16 "
-                          "MFMA products per fp32 product summed per K-step and added to an fp32 accumulator (error "
-                          "0.2-0.4x the fp32 MFMA's, tests/test_kernels_gpu.py; MMFD_FP32_GEMM=native selects the "
-                          "fp32 MFMA)" if K.fp32_gemm_mode() == 1 else "fp32 MFMA (v_mfma_f32_16x16x4f32)"),
+            "peak_memory_gb": res["peak_memory_gb"], "memory": res["memory"],
+            "fp32_gemm": ("split operands: x = hi + mid + lo bf16 planes staged together per 32-deep K-step, the six "
+                          "bf16 MFMA products per fp32 product accumulated directly into the fp32 accumulator, small "
+                          "first (error 0.62-1.14x the fp32 MFMA's, bound 1.5x in tests/test_kernels_gpu.py; "
+                          "MMFD_FP32_GEMM=native selects the fp32 MFMA)" if K.fp32_gemm_mode() == 1
+                          else "fp32 MFMA (v_mfma_f32_16x16x4f32)"),
         }
         if sec is not None:
             out["bf16"] = {"value": round(sec["pairs"], 2), "unit": "pairs/s", "ms_per_step": round(sec["ms"], 3),
@@ -875,6 +876,7 @@ def train_leg(args, dev, world, rank, precision):
     graphed = not args.no_graph and (world == 1 or os.environ.get("MMFD_DP_GRAPH", "1") == "1")
     probe = K.GemmProbe()
     torch.cuda.reset_peak_memory_stats(dev)
+    reserved0 = torch.cuda.memory_reserved(dev)
     if graphed:  # (capture runs its own eager warmup steps first)
         try:
             tr.capture(batch, warmup=max(1, args.warmup))
@@ -906,7 +908,15 @@ def train_leg(args, dev, world, rank, precision):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    peak_gb = torch.cuda.max_memory_allocated(dev) / 2**30  # the timed step's device memory high-water mark
+    # device memory: the high-water mark of allocated tensors (set by the eager steps before the
+    # capture: the graph replays run in the pool the capture reserved), and the reserved growth
+    # across capture + replays (the eager steps' cached blocks plus the graph's private pool);
+    # tools/mem_account.py separates resident / saved-for-backward / planes / graph pool
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 2**30
+    mem = {"peak_allocated_gb": round(peak_gb, 1),
+           "reserved_gb": round(torch.cuda.memory_reserved(dev) / 2**30, 1),
+           "reserved_growth_gb": round((torch.cuda.memory_reserved(dev) - reserved0) / 2**30, 1),
+           "breakdown": "profiles/r04_memory.json (tools/mem_account.py)"}
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -973,7 +983,7 @@ def train_leg(args, dev, world, rank, precision):
                        + ("; text / image encoders on two streams" if tr_conc else "")
                        + "; GEMM times from 2 eager probe steps after the timed region, encoders serialized"),
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
-            "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1)}
+            "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1), "memory": mem}
 
 
 def step_peak(precision):

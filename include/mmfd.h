@@ -178,6 +178,11 @@ typedef struct mmfd_attn_args {
      [B, Lq, H*D] buffer), written beside it — the operand of the output projection's forward and
      weight-gradient GEMMs */
   void* o_planes;
+  /* dropout keep-bitmask, uint32 [B*H*Lq][ceil(Lk/32)]: word ((b*H+h)*Lq+q)*ceil(Lk/32) + k/32, bit k%32
+     = 1 when element (q, k) is kept. With dropout_p > 0 the forward writes it when non-NULL, and the
+     backward reads it instead of re-hashing the mask when non-NULL (the same buffer, unchanged
+     between the calls); NULL: both hash (identical masks either way) */
+  uint32_t* drop_mask;
 } mmfd_attn_args;
 
 int mmfd_attn_fwd(const mmfd_attn_args* args, mmfd_stream_t stream);

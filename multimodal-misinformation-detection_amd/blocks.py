@@ -80,6 +80,9 @@ class CachedWeights:
         return r
 
 
+ATTN_DROP_MASK = os.environ.get("MMFD_ATTN_DROP_MASK") == "1"
+
+
 class StepCtx:
     def __init__(self, params: dict, dtype: torch.dtype, dropout_p: float = 0.0, seed: K.Seed | None = None,
                  training: bool = False, shadows: dict | None = None):
@@ -98,6 +101,7 @@ class StepCtx:
         self.cache_derived = False  # keep weight-derived tensors across calls (see derived())
         self._side_used = False
         self._wp = {}            # split planes of fp32 weights, by data_ptr (one split per call)
+        self._dmask = {}         # attention site -> dropout keep-bitmask (forward writes, backward reads)
 
     def enable_side_stream(self, device):
         self.side = side_stream(device)
@@ -239,6 +243,20 @@ class StepCtx:
         if self.p <= 0.0:
             return {}
         return dict(dropout_p=self.p, seed=self.seed, salt=K.salt_of(site))
+
+    def attn_drop(self, site, q=None, k=None, H=None):
+        """dropout kwargs of an attention call, plus — with MMFD_ATTN_DROP_MASK=1 — its keep-bitmask:
+        the forward call (q, k, H given) allocates the mask the kernel writes, the backward call of
+        the same site passes the same buffer and reads it instead of re-hashing. Off by default:
+        measured slower (tools/attn_bench.py, round 4: BERT fp32 fwd 369 -> 390 us, bwd 986 -> 996
+        us; bf16 162 -> 169 / 441 -> 444 us) — the backward kernels are not bound by the hash."""
+        kw = self.drop(site)
+        if not kw or not ATTN_DROP_MASK:
+            return kw
+        if q is not None:
+            self._dmask[site] = K.drop_mask_buffer(q.shape[0], H, q.shape[1], k.shape[1], q.device)
+        m = self._dmask.get(site)
+        return dict(kw, drop_mask=m) if m is not None else kw
 
     # ---- gradients -----------------------------------------------------------------------------
     def flush_ready(self):

@@ -49,7 +49,31 @@ struct AttnP {
   int idx32;  // every dropout index fits 32 bits (hash_c1)
   int vst;    // x6 backward stores as 4-column groups (16-B fp32, 8-B planes): outputs and planes aligned
   int dbg;  // x6 phase experiments (MMFD_X6A_DBG): 1 = stage zeros, 2 = skip the products
+  // dropout keep-bitmask (mmfd_attn_args::drop_mask): forward kernels that hash the mask write it,
+  // backward kernels read it instead of re-hashing; dmw = words per query row, dm_lds = the dK/dV
+  // kernel stages the head's rows in LDS (room left by its images)
+  uint32_t* dm; int dmw; int dm_lds;
 };
+
+// word ((b*H + h)*Lq + q)*dmw + k/32 of the keep-bitmask, bit k % 32 = 1 when element (q, k) is kept
+__device__ __forceinline__ uint32_t* dm_row(const AttnP& p, int64_t bh, int64_t q) { return p.dm + (bh * p.Lq + q) * p.dmw; }
+// forward, S^T layout (lane (g, li): query q0 + li, keys k0 + ks*16 + 4g + r): `kb` holds the lane's
+// keep bits of one 64-key chunk at bit ks*4 + r; the four lane groups' bits are merged by shuffles
+// into the words k0/32 and k0/32 + 1 of the query's row (all 64 lanes must be active)
+__device__ __forceinline__ void dm_write64(const AttnP& p, int64_t bh, int64_t myq, int k0, int g, uint32_t kb) {
+  uint32_t w0 = ((kb & 0xFu) << (4 * g)) | (((kb >> 4) & 0xFu) << (16 + 4 * g));
+  uint32_t w1 = (((kb >> 8) & 0xFu) << (4 * g)) | (((kb >> 12) & 0xFu) << (16 + 4 * g));
+  w0 |= __shfl_xor(w0, 16, 64);
+  w0 |= __shfl_xor(w0, 32, 64);
+  w1 |= __shfl_xor(w1, 16, 64);
+  w1 |= __shfl_xor(w1, 32, 64);
+  if (myq < p.Lq) {
+    const int w = k0 >> 5;
+    uint32_t* row = dm_row(p, bh, myq);
+    if (g == 0 && w < p.dmw) row[w] = w0;
+    if (g == 1 && w + 1 < p.dmw) row[w + 1] = w1;
+  }
+}
 
 // one fp32 gradient element into the planes at its offset in the packed buffer
 __device__ __forceinline__ void plane_put(const AttnP& p, const float* dst, float v) {
@@ -829,6 +853,19 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
           }
         }
       }
+      if (p.p > 0.f && p.dm) {
+        // the keep-bitmask for the backward, read back from P: a dropped element is 0, a kept one
+        // e * keep_scale > 0 unless exp2 underflowed — and then the backward's P of it is 0 too,
+        // so recording it as dropped changes no gradient (one register, no hash state kept live)
+        uint32_t kbits = 0;
+#pragma unroll
+        for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
+          if (ks >= nsub) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kbits |= (uint32_t)(s[ks][r] != 0.f) << (ks * 4 + r);
+        }
+        dm_write64(p, bh, myq, k0, g, kbits);
+      }
       lsum = lsum * alpha + rs;  // per-lane partial over this lane's keys; reduced at the end
       m = mnew;
 #pragma unroll
@@ -902,6 +939,12 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   float* s_lse = reinterpret_cast<float*>(smem + (DUAL ? 2 : 4) * img);
   float* s_delta = s_lse + V2_LMAX;
   float* kbias = s_delta + V2_LMAX;
+  uint32_t* s_dm = reinterpret_cast<uint32_t*>(kbias + V2_LMAX);  // dm_lds: the head's keep-bitmask rows
+  if (p.dm_lds) {
+    const uint32_t* src = dm_row(p, bh, 0);
+    const int nw = (int)p.Lq * p.dmw;
+    for (int i = tid; i < lq_pad * p.dmw; i += NTH) s_dm[i] = i < nw ? src[i] : 0u;
+  }
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
   stage_all<T, D, false, NTH>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
@@ -979,7 +1022,12 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
         const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
         if (p.p > 0.f) {  // one uniform branch per subtile; the element index advances by Lk per query
-          if (p.idx32) {
+          if (p.dm_lds) {  // bit mykey of the query rows' words (LDS broadcast reads)
+            const uint32_t* col = s_dm + (mykey >> 5);
+            const int sh = (int)(mykey & 31);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] = ((col[(qs * 16 + 4 * g + r) * p.dmw] >> sh) & 1u) ? p.keep_scale : 0.f;
+          } else if (p.idx32) {
             const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
             const uint32_t c = ((uint32_t)hcol + (uint32_t)(qs * 16 + 4 * g) * (uint32_t)p.Lk) * HASH_C1;
 #pragma unroll
@@ -1086,6 +1134,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
     }
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
+    const uint32_t* dmrow = p.dm ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1103,6 +1152,8 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
       }
     }
     for (int kc2 = 0; kc2 < nkc; ++kc2) {
+      // the keep word of this chunk's keys (dropout bitmask), loaded ahead of the products
+      const uint32_t kw = (p.p > 0.f && p.dm) ? dmrow[(SUBS * kc2) >> 1] : 0u;
       uint4 tk[C::DT];  // transposed K fragments (B operand of dQ)
       if constexpr (PF) {
 #pragma unroll
@@ -1144,7 +1195,10 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
         const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
         if (p.p > 0.f) {  // one uniform branch per subtile
-          if (p.idx32) {
+          if (p.dm) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] = ((kw >> ((ks & 1) * 16 + 4 * g + r)) & 1u) ? p.keep_scale : 0.f;
+          } else if (p.idx32) {
             const uint32_t c = ((uint32_t)hrow + (uint32_t)(ks * 16 + 4 * g)) * HASH_C1;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -1475,13 +1529,16 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
       }
       if constexpr (DROP) {
         const uint32_t cc = rowc1 + (uint32_t)k0 * HASH_C1;
+        uint32_t kbits = 0;
 #pragma unroll
         for (int ks = 0; ks < NS; ++ks)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t hsh = hash_c1(hkey, cc + (uint32_t)(ks * 16 + r) * HASH_C1);
-            s[ks][r] = (hsh < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
+            const bool kp = hash_c1(hkey, cc + (uint32_t)(ks * 16 + r) * HASH_C1) >= p.thr;
+            s[ks][r] = kp ? s[ks][r] * p.keep_scale : 0.f;
+            kbits |= (uint32_t)kp << (ks * 4 + r);
           }
+        if (p.dm) dm_write64(p, bh, myq, k0, g, kbits);  // the backward kernels read it
       }
       lsum = lsum * alpha + rs;
       m = mnew;
@@ -1598,7 +1655,8 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
   X6A_STAMP(9);
 }
 
-template <int D, bool DROP>
+// DROP (dK/dV, dQ): 0 = none, 1 = re-hash the forward's mask, 2 = read the forward's keep-bitmask
+template <int D, int DROP>
 __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   // Q/dO planes of the head resident (+ lse, delta, key bias); each wave owns 16 keys
   constexpr int KCH = D / 32, DT = D / 16;
@@ -1613,8 +1671,14 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   float* s_lse = reinterpret_cast<float*>(smem + 6 * img);
   float* s_delta = s_lse + lq16;
   float* kbias = s_delta + lq16;
+  uint32_t* s_dm = reinterpret_cast<uint32_t*>(kbias + lk16);  // DROP == 2: the head's keep-bitmask rows
   const float* kb = reinterpret_cast<const float*>(p.k) + b * p.k_sb + h * p.D;
   const float* vb = reinterpret_cast<const float*>(p.v) + b * p.v_sb + h * p.D;
+  if constexpr (DROP == 2) {
+    const uint32_t* src = dm_row(p, bh, 0);
+    const int nw = (int)p.Lq * p.dmw;
+    for (int i = tid; i < lq16 * p.dmw; i += V2_THREADS) s_dm[i] = i < nw ? src[i] : 0u;
+  }
   X6Row<KCH> kn, vn;  // the wave's first key block, raw (loaded with the staging)
   x6_row_load<KCH>(kn, kb, p.k_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
   x6_row_load<KCH>(vn, vb, p.v_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
@@ -1684,7 +1748,7 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
       for (int h2 = 0; h2 < NS; ++h2)
 #pragma unroll
         for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
-      if constexpr (DROP) {  // the element index advances by Lk per query
+      if constexpr (DROP == 1) {  // the element index advances by Lk per query
 #pragma unroll
         for (int h2 = 0; h2 < NS; ++h2)
 #pragma unroll
@@ -1692,6 +1756,14 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
             const uint32_t e = colc1 + (uint32_t)((2 * qc + h2) * 16 + r) * lkc1;
             z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
           }
+      } else if constexpr (DROP == 2) {  // bit mykey of the query rows' words (LDS broadcast reads)
+        const uint32_t* col = s_dm + (mykey >> 5);
+        const int sh = (int)(mykey & 31);
+#pragma unroll
+        for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            z[h2][r] = ((col[((2 * qc + h2) * 16 + 4 * g + r) * p.dmw] >> sh) & 1u) ? p.keep_scale : 0.f;
       }
 #pragma unroll
       for (int h2 = 0; h2 < NS; ++h2) {
@@ -1819,7 +1891,7 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
   }
 }
 
-template <int D, bool DROP>
+template <int D, int DROP>
 __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
   // K/V planes of the head resident; each wave owns 16 queries: dQ = dS K
   constexpr int KCH = D / 32, DT = D / 16;
@@ -1873,8 +1945,11 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
     if (wdelta && g == 0 && myq < p.Lq) p.delta[bh * p.Lq + myq] = dsum;
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    const uint32_t* dmrow = DROP == 2 ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
     auto chunk = [&](int kc2, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-key subtiles of this 32-key chunk
+      uint32_t kw = 0;  // DROP == 2: the chunk's keep word (32 keys), loaded ahead of the products
+      if constexpr (DROP == 2) kw = dmrow[kc2];
       f32x4 sd[4];  // S^T (even) and dP^T (odd) per subtile
 #pragma unroll
       for (int i = 0; i < 4; ++i) sd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1907,7 +1982,7 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
       for (int h2 = 0; h2 < NS; ++h2)
 #pragma unroll
         for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
-      if constexpr (DROP) {
+      if constexpr (DROP == 1) {
 #pragma unroll
         for (int h2 = 0; h2 < NS; ++h2)
 #pragma unroll
@@ -1915,6 +1990,11 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
             const uint32_t e = rowc1 + (uint32_t)((2 * kc2 + h2) * 16 + r) * HASH_C1;
             z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
           }
+      } else if constexpr (DROP == 2) {
+#pragma unroll
+        for (int h2 = 0; h2 < NS; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[h2][r] = ((kw >> (h2 * 16 + 4 * g + r)) & 1u) ? p.keep_scale : 0.f;
       }
 #pragma unroll
       for (int h2 = 0; h2 < NS; ++h2) {
@@ -2047,17 +2127,24 @@ void launch_fwd_x6_d(const AttnP& p, hipStream_t s) {
                      6 * lk16 * X6A_RB + lk16 * 4, s, p);
 }
 
-template <int D, bool DROP>
+constexpr int X6A_LDS_MAX = 160 * 1024;
+// the dK/dV kernel's LDS, with the head's keep-bitmask rows when `dm`
+int x6_dkdv_lds(const AttnP& p, bool dm) {
+  const int lq16 = v2_pad(p.Lq, 16), lk16 = v2_pad(p.Lk, 16);
+  return 6 * lq16 * X6A_RB + (2 * lq16 + lk16) * 4 + (dm ? lq16 * p.dmw * 4 : 0);
+}
+
+template <int D, int DQD, int DKD>
 void launch_bwd_x6_d(const AttnP& p, hipStream_t s) {
-  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_x6_kernel<D, DROP>), X6A_LDS),
-                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_x6_kernel<D, DROP>), X6A_LDS), true);
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_x6_kernel<D, DKD>), X6A_LDS_MAX),
+                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_x6_kernel<D, DQD>), X6A_LDS), true);
   (void)once;
   // dQ first: it computes delta = rowsum(dO * O) for dK/dV (no separate delta pass)
-  const int lq16 = v2_pad(p.Lq, 16), lk16 = v2_pad(p.Lk, 16);
-  hipLaunchKernelGGL((attn_dq_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+  const int lk16 = v2_pad(p.Lk, 16);
+  hipLaunchKernelGGL((attn_dq_x6_kernel<D, DQD>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
                      6 * lk16 * X6A_RB + lk16 * 4, s, p);
-  hipLaunchKernelGGL((attn_dkdv_x6_kernel<D, DROP>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
-                     6 * lq16 * X6A_RB + (2 * lq16 + lk16) * 4, s, p);
+  hipLaunchKernelGGL((attn_dkdv_x6_kernel<D, DKD>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS),
+                     x6_dkdv_lds(p, DKD == 2), s, p);
 }
 
 // dropout as a template argument: a run-time flag let the compiler if-convert the hash into every
@@ -2067,10 +2154,19 @@ void launch_fwd_x6(const AttnP& p, hipStream_t s) {
   if (p.D > 32) { if (dr) launch_fwd_x6_d<64, true>(p, s); else launch_fwd_x6_d<64, false>(p, s); }
   else { if (dr) launch_fwd_x6_d<32, true>(p, s); else launch_fwd_x6_d<32, false>(p, s); }
 }
+// dropout in the backward: the forward's keep-bitmask when the caller kept one (dQ reads its row
+// words from memory; dK/dV stages the head's rows in LDS when they fit beside its images, else
+// re-hashes), otherwise the hash again
+template <int D>
+void launch_bwd_x6_dd(const AttnP& p, hipStream_t s) {
+  if (p.p <= 0.f) return launch_bwd_x6_d<D, 0, 0>(p, s);
+  if (!p.dm) return launch_bwd_x6_d<D, 1, 1>(p, s);
+  if (x6_dkdv_lds(p, true) <= X6A_LDS_MAX) return launch_bwd_x6_d<D, 2, 2>(p, s);
+  launch_bwd_x6_d<D, 2, 1>(p, s);
+}
 void launch_bwd_x6(const AttnP& p, hipStream_t s) {
-  const bool dr = p.p > 0.f;
-  if (p.D > 32) { if (dr) launch_bwd_x6_d<64, true>(p, s); else launch_bwd_x6_d<64, false>(p, s); }
-  else { if (dr) launch_bwd_x6_d<32, true>(p, s); else launch_bwd_x6_d<32, false>(p, s); }
+  if (p.D > 32) launch_bwd_x6_dd<64>(p, s);
+  else launch_bwd_x6_dd<32>(p, s);
 }
 
 int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
@@ -2119,7 +2215,26 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.pl = nullptr; p.pl_only = 0;
   static const int dbg = getenv("MMFD_X6A_DBG") ? atoi(getenv("MMFD_X6A_DBG")) : 0;
   p.dbg = dbg;
+  p.dm = p.p > 0.f ? a.drop_mask : nullptr;
+  p.dmw = (int)((a.Lk + 31) / 32);
+  p.dm_lds = 0;
+  MMFD_CHECK_ARG(!p.dm || ((uintptr_t)p.dm & 3) == 0, "attn: drop_mask must be 4-B aligned");
   return 0;
+}
+
+// the keep-bitmask from the hash, for forward kernels that do not write it (the streaming v1 path)
+__global__ void dm_fill_kernel(AttnP p) {
+  const int64_t words = p.B * p.H * p.Lq * p.dmw;
+  const uint32_t hkey = mmfd_hash_key(*p.seed, p.salt);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / p.dmw, w = i - row * p.dmw;  // row = bh * Lq + q
+    uint32_t bits = 0;
+    for (int j = 0; j < 32; ++j) {
+      const int64_t k = w * 32 + j;
+      if (k < p.Lk && mmfd_hash_k(hkey, (uint64_t)(row * p.Lk + k)) >= p.thr) bits |= 1u << j;
+    }
+    p.dm[i] = bits;
+  }
 }
 
 template <typename T, int D, int HPB, bool REL>
@@ -2162,17 +2277,21 @@ void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
   constexpr int RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
   const int lq_pad = v2_pad(p.Lq, v2_kc<T>()), lk_pad = v2_pad(p.Lk, v2_kc<T>());
   constexpr int NI1 = V2<T, D>::DUAL ? 2 : 4, NI2 = V2<T, D>::DUAL ? 2 : 3;  // LDS images per kernel
-  const int lds1 = NI1 * lq_pad * RB + 3 * V2_LMAX * 4;
+  const int lds1n = NI1 * lq_pad * RB + 3 * V2_LMAX * 4;
   const int lds2 = NI2 * lk_pad * RB + lk_pad * 4;
-  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH, REL>),
-                                   NI1 * V2_LMAX * RB + 3 * V2_LMAX * 4),
+  constexpr int lds1_max = NI1 * V2_LMAX * RB + 3 * V2_LMAX * 4 + V2_LMAX * (V2_LMAX / 32) * 4;
+  static_assert(lds1_max <= 160 * 1024, "dK/dV LDS");
+  AttnP q = p;  // dK/dV stages the head's keep-bitmask rows in LDS when the caller kept them
+  q.dm_lds = p.p > 0.f && p.dm && lds1n + lq_pad * p.dmw * 4 <= lds1_max;
+  const int lds1 = lds1n + (q.dm_lds ? lq_pad * p.dmw * 4 : 0);
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH, REL>), lds1_max),
                       set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D, REL>),
                                    NI2 * V2_LMAX * RB + V2_LMAX * 4),
                       true);
   (void)once;
   // dQ first: it writes delta = rowsum(dO * O) for dK/dV (no separate delta pass)
-  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, p);
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, p);
+  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, q);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, q);
 }
 
 template <typename T, int D>
@@ -2233,6 +2352,11 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   else if (a->dtype == MMFD_BF16) { if (a->D > 32) launch_fwd<bf16, 64>(p, s); else launch_fwd<bf16, 32>(p, s); }
   else { if (a->D > 32) launch_fwd<float, 64>(p, s); else launch_fwd<float, 32>(p, s); }
   MMFD_CHECK_LAUNCH("attn_fwd");
+  if (p.dm && !v2) {  // the streaming kernels hash without writing the mask: fill it for the backward
+    const int64_t words = p.B * p.H * p.Lq * p.dmw;
+    hipLaunchKernelGGL(dm_fill_kernel, dim3((unsigned)std::min<int64_t>((words + 255) / 256, 8192)), dim3(256), 0, s, p);
+    MMFD_CHECK_LAUNCH("attn_fwd dm_fill");
+  }
   if (a->o_planes && !v2)  // the streaming kernels write fp32 only: split afterwards
     return mmfd_split3(p.B * p.Lq, W, (const float*)a->o, W, a->o_planes, stream);
   return 0;

@@ -159,11 +159,21 @@ mmfd_attn_args attn_args(const at::Tensor& q, const at::Tensor& k, const at::Ten
   return a;
 }
 
+// the dropout keep-bitmask buffer: int32 (uint32 words) [B*H*Lq*ceil(Lk/32)], contiguous, on the device
+uint32_t* drop_mask_ptr(const std::optional<at::Tensor>& m, const mmfd_attn_args& a) {
+  if (!m.has_value() || !m->defined()) return nullptr;
+  TORCH_CHECK(m->scalar_type() == at::kInt && m->is_contiguous() && m->is_cuda() &&
+                  m->numel() == a.B * a.H * a.Lq * ((a.Lk + 31) / 32),
+              "mmfd attention: drop_mask must be a contiguous int32 device tensor of B*H*Lq*ceil(Lk/32) words");
+  return reinterpret_cast<uint32_t*>(m->data_ptr());
+}
+
 void attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out, at::Tensor& lse,
               int64_t heads, double scale, const std::optional<at::Tensor>& key_bias,
               const std::optional<at::Tensor>& rel_bias, int64_t rel_bias_sb, int64_t rel_bias_mod, double dropout_p,
               const std::optional<at::Tensor>& seed, int64_t salt, const std::optional<at::Tensor>& cos_logit_scale,
-              double cos_max_log, const std::optional<at::Tensor>& o_planes = std::nullopt) {
+              double cos_max_log, const std::optional<at::Tensor>& o_planes = std::nullopt,
+              const std::optional<at::Tensor>& drop_mask = std::nullopt) {
   mmfd_attn_args a = attn_args(q, k, v, heads, scale, key_bias, rel_bias, rel_bias_sb, rel_bias_mod, dropout_p, seed, salt);
   const void* p;
   head_view(out, "out", &p, &a.o_sb, &a.o_st); a.o = const_cast<void*>(p);
@@ -175,6 +185,7 @@ void attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at:
                 "mmfd::attn_fwd: o_planes must be contiguous bf16 [3, B*L, H*D]");
     a.o_planes = o_planes->data_ptr();
   }
+  a.drop_mask = drop_mask_ptr(drop_mask, a);
   check(mmfd_attn_fwd(&a, stream_of(q)), "mmfd::attn_fwd");
 }
 
@@ -183,7 +194,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
               const std::optional<at::Tensor>& key_bias, const std::optional<at::Tensor>& rel_bias, int64_t rel_bias_sb,
               int64_t rel_bias_mod, double dropout_p, const std::optional<at::Tensor>& seed, int64_t salt,
               bool accumulate_dq, bool accumulate_dkv, const std::optional<at::Tensor>& dqkv_planes = std::nullopt,
-              bool planes_only = false) {
+              bool planes_only = false, const std::optional<at::Tensor>& drop_mask = std::nullopt) {
   mmfd_attn_args a = attn_args(q, k, v, heads, scale, key_bias, rel_bias, rel_bias_sb, rel_bias_mod, dropout_p, seed, salt);
   const void* p;
   head_view(o, "o", &p, &a.o_sb, &a.o_st); a.o = const_cast<void*>(p);
@@ -202,6 +213,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     a.dqkv_planes = dqkv_planes->data_ptr();
     a.planes_only = planes_only ? 1 : 0;
   }
+  a.drop_mask = drop_mask_ptr(drop_mask, a);
   check(mmfd_attn_bwd(&a, stream_of(q)), "mmfd::attn_bwd");
 }
 
@@ -326,11 +338,11 @@ TORCH_LIBRARY(mmfd, m) {
   m.def("linear(Tensor x, Tensor w, Tensor? bias, int act=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) out, Tensor(b!) lse, int heads, float scale, "
         "Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, float dropout_p, Tensor? seed, int salt, "
-        "Tensor? cos_logit_scale, float cos_max_log, Tensor(c!)? o_planes=None) -> ()");
+        "Tensor? cos_logit_scale, float cos_max_log, Tensor(c!)? o_planes=None, Tensor(d!)? drop_mask=None) -> ()");
   m.def("attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dout, Tensor(a!) dq, Tensor(b!) dk, "
         "Tensor(c!) dv, int heads, float scale, Tensor? key_bias, Tensor? rel_bias, int rel_bias_sb, int rel_bias_mod, "
         "float dropout_p, Tensor? seed, int salt, bool accumulate_dq, bool accumulate_dkv, "
-        "Tensor(d!)? dqkv_planes=None, bool planes_only=False)-> ()");
+        "Tensor(d!)? dqkv_planes=None, bool planes_only=False, Tensor? drop_mask=None)-> ()");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, Tensor(a!) y, Tensor(b!) mean, "
         "Tensor(c!) rstd, Tensor(d!)? planes=None) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor? dx_add, "

@@ -153,7 +153,7 @@ def bert_forward(ctx: Bk.StepCtx, cfg: BertConfig, ids, mask, tts, keep, site="b
         qkv = Bk.linear_packed(ctx, x, [p + ".attention.self.query", p + ".attention.self.key",
                                         p + ".attention.self.value"], xp=xp).view(B, L, 3 * D)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
-        attn_drop = dict(ctx.drop(s + ".attn")) if cfg.attention_probs_dropout_prob > 0 else {}
+        attn_drop = dict(ctx.attn_drop(s + ".attn", q, k, H)) if cfg.attention_probs_dropout_prob > 0 else {}
         # the output's planes from the attention kernel itself (fp32 split-operand mode)
         op = Bk.new_planes(ctx, B * L, D, q.device) if keep else None
         o, lse = K.attn_fwd(q, k, v, H, key_bias=kb, o_planes=op, **attn_drop)

@@ -43,7 +43,7 @@ def _attn_ln_fwd(ctx, cfg, q, k, v, res2d, out_name, ln_name, site, want_planes=
     """(y, y planes or None, state)"""
     B, Lq, _ = q.shape
     op = Bk.new_planes(ctx, B * Lq, q.shape[2], q.device)
-    o, lse = K.attn_fwd(q, k, v, cfg.H, o_planes=op, **ctx.drop(site + ".attn"))
+    o, lse = K.attn_fwd(q, k, v, cfg.H, o_planes=op, **ctx.attn_drop(site + ".attn", q, k, cfg.H))
     s, _ = Bk.linear(ctx, Bk.as2d(o), out_name, residual=res2d, xp=op)
     y, mean, rstd, yp = Bk.layernorm_planes(ctx, s, ln_name, cfg.eps, want=want_planes)
     return y, yp, (q, k, v, o, op, lse, s, mean, rstd, out_name, ln_name, site)
@@ -66,7 +66,7 @@ def _attn_ln_bwd(ctx, cfg, dy2d, st, *, dq=None, acc_dq=False, dk=None, dv=None,
     q, k, v, o, op, lse, s, mean, rstd, out_name, ln_name, site = st
     ds, do = _attn_ln_out_bwd(ctx, dy2d, st)
     K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dq, dk=dk, dv=dv, accumulate_dq=acc_dq, accumulate_dkv=acc_dkv,
-               dqkv_planes=dqkv_planes, **ctx.drop(site + ".attn"))
+               dqkv_planes=dqkv_planes, **ctx.attn_drop(site + ".attn"))
     return ds
 
 
@@ -115,7 +115,7 @@ def _repr_modality_bwd(ctx, cfg, dY2d, st, need_dxin, out=None):
         ds2, do2 = _attn_ln_out_bwd(ctx, dC, st["st2"])      # ds2: dH (residual part)
         # dq of the cross attention goes straight into dH (= ds2), dk/dv start dQKV's K|V blocks
         K.attn_bwd(q2, k2, v2, o2, lse2, do2, cfg.H, dq=ds2.view(B, L, E), dk=dqkv[..., E:2 * E],
-                   dv=dqkv[..., 2 * E:], accumulate_dq=True, accumulate_dkv=False, **ctx.drop(site2 + ".attn"))
+                   dv=dqkv[..., 2 * E:], accumulate_dq=True, accumulate_dkv=False, **ctx.attn_drop(site2 + ".attn"))
         dX = _attn_ln_bwd(ctx, cfg, ds2, st["st1"], dq=dqkv[..., :E], dk=dqkv[..., E:2 * E], dv=dqkv[..., 2 * E:],
                           acc_dkv=True, dqkv_planes=dqkvp)
     else:
@@ -243,7 +243,7 @@ def _path_bwd(ctx, cfg, path, dS, cst, dH, dQ, dKV):
     if first_kv:
         dKV[em] = torch.empty_like(cst["KV"][em])
     K.attn_bwd(q, k, v, o, lse, do, cfg.H, dq=dQ[hm], dk=dKV[em][..., :E], dv=dKV[em][..., E:],
-               accumulate_dq=not first_q, accumulate_dkv=not first_kv, **ctx.drop(site + ".attn"))
+               accumulate_dq=not first_q, accumulate_dkv=not first_kv, **ctx.attn_drop(site + ".attn"))
 
 
 def _q_bwd(ctx, cfg, hm, dq, cst, dH):

@@ -93,6 +93,7 @@ class AttnArgs(ctypes.Structure):
         ("cos_max_log", ctypes.c_float),
         ("dqkv_planes", ctypes.c_void_p), ("planes_only", ctypes.c_int),
         ("o_planes", ctypes.c_void_p),
+        ("drop_mask", ctypes.c_void_p),
     ]
 
 
@@ -509,10 +510,17 @@ def _head_view(t, H, D):
     return t.data_ptr(), t.stride(0), t.stride(1)
 
 
+def drop_mask_buffer(B, H, Lq, Lk, device):
+    """the dropout keep-bitmask of one attention call (include/mmfd.h mmfd_attn_args.drop_mask): int32
+    words [B*H*Lq*ceil(Lk/32)], written by attn_fwd and read by attn_bwd instead of re-hashing"""
+    return torch.empty(B * H * Lq * ((Lk + 31) // 32), device=device, dtype=torch.int32)
+
+
 def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, dropout_p=0.0, seed=None, salt=0,
-             cos_logit_scale=None, cos_max_log=0.0, o_planes=None):
+             cos_logit_scale=None, cos_max_log=0.0, o_planes=None, drop_mask=None):
     """q: [B, Lq, H*D], k/v: [B, Lk, H*D] (views into fused QKV buffers are fine).
     cos_logit_scale (fp32 [H], bf16 only): Swinv2 cosine attention, q/k normalised in the kernel.
+    drop_mask (drop_mask_buffer, with dropout_p > 0): receives the keep-bitmask for attn_bwd.
     Returns (o [B, Lq, H*D], lse [B, H, Lq] fp32)."""
     _require_cuda(q, k, v)
     B, Lq, HD = q.shape
@@ -527,7 +535,8 @@ def attn_fwd(q, k, v, H, *, out=None, scale=None, key_bias=None, rel_bias=None, 
         raise ValueError("cos_logit_scale must be a contiguous fp32 tensor of H values")
     _ops().attn_fwd(q, k, v, out, lse, int(H), float(scale if scale is not None else D ** -0.5), key_bias,
                     rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
-                    seed.t if seed is not None else None, _salt(salt), cos_logit_scale, float(cos_max_log), o_planes)
+                    seed.t if seed is not None else None, _salt(salt), cos_logit_scale, float(cos_max_log), o_planes,
+                    drop_mask if dropout_p > 0 else None)
     return out, lse
 
 
@@ -583,7 +592,7 @@ def attn_fill_masked_rows(v, o, H, mask):
 
 def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None, key_bias=None, rel_bias=None,
              dropout_p=0.0, seed=None, salt=0, accumulate_dq=False, accumulate_dkv=False, dqkv_planes=None,
-             planes_only=False):
+             planes_only=False, drop_mask=None):
     """dq, dk, dv (views of one packed [B, L, 3*H*D] buffer when `dqkv_planes` is given: bf16
     [3, B*L, 3*H*D] split planes of that buffer, written by the kernels; planes_only skips the
     fp32 stores — for a gradient read only by split-operand GEMMs, see x6_ok)"""
@@ -600,7 +609,7 @@ def attn_bwd(q, k, v, o, lse, dout, H, *, dq=None, dk=None, dv=None, scale=None,
     _ops().attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, int(H), float(scale if scale is not None else D ** -0.5),
                     key_bias, rel_bias if rb is not None else None, int(rb_sb), int(rb_mod), float(dropout_p),
                     seed.t if seed is not None else None, _salt(salt), bool(accumulate_dq), bool(accumulate_dkv),
-                    dqkv_planes, bool(planes_only))
+                    dqkv_planes, bool(planes_only), drop_mask if dropout_p > 0 else None)
     return dq, dk, dv
 
 

@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from . import blocks as Bk
 from . import kernels as K
 
 _COUNT = {"mlp": 0, "mha": 0}
@@ -79,6 +80,8 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, Q, Kt, V, H, p, seed, site):
         kw = dict(dropout_p=p, seed=seed, salt=K.salt_of(site)) if p > 0 else {}
         q, k, v = Q.contiguous(), Kt.contiguous(), V.contiguous()
+        if kw and Bk.ATTN_DROP_MASK:  # the forward's keep-bitmask, read by the backward (blocks.StepCtx.attn_drop)
+            kw["drop_mask"] = K.drop_mask_buffer(q.shape[0], H, q.shape[1], k.shape[1], q.device)
         o, lse = K.attn_fwd(q, k, v, H, **kw)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.meta = (H, kw)

@@ -763,3 +763,51 @@ def test_gemm_single_tile_weight_gradient_many_splits(dtype):
     tol = (1e-5 if dtype == torch.float32 else 2e-3) * ref.abs().max().item()
     assert (dw.double() - ref).abs().max().item() <= tol
     assert (rs.double() - (0.25 + dy.double().sum(0))).abs().max().item() <= 1e-4 * math.sqrt(Kd)
+
+
+def _pack_keep_bits(keep, Lk):
+    """oracle keep mask [B, H, Lq, Lk] (bool) -> the drop_mask words [B*H*Lq, ceil(Lk/32)] (uint32)"""
+    import numpy as np
+    W = (Lk + 31) // 32
+    k = np.zeros(keep.shape[:-1] + (W * 32,), dtype=np.uint64)
+    k[..., :Lk] = keep
+    k = k.reshape(-1, W, 32)
+    return (k << np.arange(32, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,H,L,D", [(4, 12, 128, 64), (3, 8, 197, 32), (2, 4, 300, 64)])
+def test_attention_dropout_keep_bitmask(dtype, B, H, L, D):
+    """the forward writes the dropout keep-mask once as a bitmask
+    (mmfd_attn_args.drop_mask) and the backward reads it instead of re-hashing. The words equal the
+    oracle's counter-hash mask (oracle/dropout_hash.keep_mask) bit for bit on every valid key, and
+    output, lse, dQ, dK and dV are bit-identical with and without the mask — BERT's shape (the
+    split-operand / bf16 resident kernels, mask staged in LDS by dK/dV), the head's D = 32 at
+    L = 197 (fp32: dK/dV has no LDS left for the mask and re-hashes), and L = 300 (the streaming
+    kernels, whose forward does not hash into the mask: a fill pass writes it)."""
+    import numpy as np
+    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    g = torch.Generator(DEV).manual_seed(B * 1000 + L)
+    q = torch.randn(B, L, H * D, generator=g, device=DEV).to(dt)
+    kv = torch.randn(B, L, 2 * H * D, generator=g, device=DEV).to(dt)
+    do = torch.randn(B, L, H * D, generator=g, device=DEV).to(dt)
+    lens = torch.randint(L // 2, L + 1, (B,), generator=torch.Generator().manual_seed(L))
+    kb = torch.where(torch.arange(L)[None] < lens[:, None], 0.0, -10000.0).to(DEV)
+    p, seed, salt = 0.1, K.Seed(91), K.salt_of("test.attn.bitmask")
+    k, v = kv[..., :H * D], kv[..., H * D:]
+    res = {}
+    for use in (False, True):
+        dm = K.drop_mask_buffer(B, H, L, L, DEV) if use else None
+        o, lse = K.attn_fwd(q, k, v, H, key_bias=kb, dropout_p=p, seed=seed, salt=salt, drop_mask=dm)
+        dq, dk, dv = K.attn_bwd(q, k, v, o, lse, do, H, key_bias=kb, dropout_p=p, seed=seed, salt=salt, drop_mask=dm)
+        torch.cuda.synchronize()
+        res[use] = (o, lse, dq, dk, dv, dm)
+    for a, b in zip(res[False][:5], res[True][:5]):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
+    words = res[True][5].cpu().numpy().view(np.uint32).reshape(B, H * L, -1)
+    want = _pack_keep_bits(keep_mask(91, salt, (B, H, L, L), p), L).reshape(B, H * L, -1)
+    # compared on the keys a query attends to (the bf16 resident forward records the mask from P,
+    # whose masked-out keys are 0 whatever the hash: their backward P is 0 as well)
+    for b in range(B):
+        valid = _pack_keep_bits(np.arange(L)[None, None, None, :] < int(lens[b]), L).reshape(-1)
+        assert np.array_equal(words[b] & valid, want[b] & valid), b

@@ -1,5 +1,6 @@
 """Attention kernels at the encoder shapes (bs=256 pairs -> 512 sequences x 12 heads, D=64):
 BERT L=128 with key mask + dropout 0.1, ViT L=197 without. Prints per-kernel-call times.
+BERT runs twice: the backward re-hashing the dropout mask, and reading the forward's keep-bitmask.
 python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native] [--planes]"""
 import argparse
 import os
@@ -12,7 +13,7 @@ import mmfd  # noqa: E402
 from mmfd import kernels as K  # noqa: E402
 
 
-def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False):
+def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False, bitmask=False):
     B, H, D = 512, 12, 64
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -26,6 +27,8 @@ def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False):
         kb = K.mask_to_bias(mask.to(dev))
     seed = K.Seed(5)
     kw = dict(key_bias=kb, dropout_p=p, seed=seed, salt=K.salt_of("bench")) if p > 0 else dict(key_bias=kb)
+    if p > 0 and bitmask:  # the forward writes the keep-bitmask, the backward reads it
+        kw["drop_mask"] = K.drop_mask_buffer(B, H, L, L, dev)
     o, lse = K.attn_fwd(q, k, v, H, **kw)
     dq = torch.empty_like(q); dk = torch.empty_like(k); dv = torch.empty_like(v)
     fkw, bkw = {}, {}
@@ -70,6 +73,8 @@ if __name__ == "__main__":
     for dt in a.dtype.split(","):
         t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
         if a.only in ("", "bert"):
-            case(f"{dt} bert L=128 mask p={a.bert_p}", 128, True, a.bert_p, a.iters, t, a.planes)
+            case(f"{dt} bert L=128 mask p={a.bert_p} hash   ", 128, True, a.bert_p, a.iters, t, a.planes)
+            if a.bert_p > 0:
+                case(f"{dt} bert L=128 mask p={a.bert_p} bitmask", 128, True, a.bert_p, a.iters, t, a.planes, True)
         if a.only in ("", "vit"):
             case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t, a.planes)
