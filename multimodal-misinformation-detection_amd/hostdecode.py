@@ -13,32 +13,21 @@ per-image work is that copy and the GPU preprocessing's copy into its pinned upl
 from __future__ import annotations
 
 import os
-from multiprocessing import resource_tracker, shared_memory
+import sys
+from multiprocessing import shared_memory
+from multiprocessing import util as mp_util
 
 import numpy as np
 
+# the worker functions live in a torch-free top-level module (see mmfd_decode_worker.py)
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+if _PKG_DIR not in sys.path:
+    sys.path.append(_PKG_DIR)
+import mmfd_decode_worker as _dw  # noqa: E402
 
-def _decode_group(paths):
-    """worker: decode `paths` -> (shm name or None, [(h, w, byte offset)])"""
-    from PIL import Image
-    arrs = []
-    for p in paths:
-        with Image.open(p) as im:
-            arrs.append(np.asarray(im.convert("RGB"), dtype=np.uint8))
-    total = sum(a.nbytes for a in arrs)
-    if total == 0:
-        return None, [(a.shape[0], a.shape[1], 0) for a in arrs]
-    shm = shared_memory.SharedMemory(create=True, size=total)
-    # the caller owns (and unlinks) the block: keep this process's resource tracker out of it
-    resource_tracker.unregister(shm._name, "shared_memory")
-    meta, off = [], 0
-    for a in arrs:
-        np.frombuffer(shm.buf, dtype=np.uint8, count=a.nbytes, offset=off)[:] = a.reshape(-1)
-        meta.append((a.shape[0], a.shape[1], off))
-        off += a.nbytes
-    name = shm.name
-    shm.close()
-    return name, meta
+
+def _shutdown_executor(ex):
+    ex.shutdown(wait=True, cancel_futures=True)
 
 
 class DecodePool:
@@ -51,12 +40,16 @@ class DecodePool:
         self.group = max(1, int(group))
         ctx = mp.get_context("forkserver")
         # the workers fork from a server that imported this module (and numpy / PIL) once
-        ctx.set_forkserver_preload([__name__, "PIL.Image"])
+        ctx.set_forkserver_preload(["mmfd_decode_worker", "PIL.Image"])
         self._ex = cf.ProcessPoolExecutor(max_workers=self.workers, mp_context=ctx)
+        # shut the workers down before the process's exit joins its children: in a multiprocessing
+        # child (a corpus-build rank) the exit joins them before concurrent.futures' own exit hook
+        # has told them to stop — a hang whenever the pool was still alive at that point
+        self._fin = mp_util.Finalize(self, _shutdown_executor, args=(self._ex,), exitpriority=10)
 
     def submit(self, paths):
         paths = list(paths)
-        return [self._ex.submit(_decode_group, paths[i:i + self.group]) for i in range(0, len(paths), self.group)]
+        return [self._ex.submit(_dw.decode_group, paths[i:i + self.group]) for i in range(0, len(paths), self.group)]
 
     @staticmethod
     def get(handle):
@@ -70,7 +63,6 @@ class DecodePool:
                 out += [np.zeros((h, w, 3), np.uint8) for h, w, _ in meta]
                 continue
             shm = shared_memory.SharedMemory(name=name)
-            resource_tracker.unregister(shm._name, "shared_memory")  # attached, not created here
             try:
                 src = np.frombuffer(shm.buf, dtype=np.uint8)
                 block = src.copy()
@@ -83,38 +75,23 @@ class DecodePool:
         return out, (lambda: None)
 
     def close(self):
-        self._ex.shutdown(wait=True, cancel_futures=True)
-
-    def __del__(self):
-        try:
-            self._ex.shutdown(wait=False, cancel_futures=True)
-        except Exception:
-            pass
+        self._fin()  # (runs once)
 
 
 # ---- decode straight into page-locked shared memory (no host copies in the caller) -------------------
-_ATTACHED = {}
-
-
-def _decode_group_into(shm_name, base, cap, paths):
-    """worker: decode `paths` into the shared ring at [base, base + cap), packed back to back ->
-    [(h, w, offset from base)] with offset -1 and the pixels themselves for an image past the space"""
-    from PIL import Image
-    shm = _ATTACHED.get(shm_name)
-    if shm is None:
-        shm = _ATTACHED[shm_name] = shared_memory.SharedMemory(name=shm_name)
-        resource_tracker.unregister(shm._name, "shared_memory")
-    out, off = [], 0
-    for p in paths:
-        with Image.open(p) as im:
-            a = np.asarray(im.convert("RGB"), dtype=np.uint8)
-        if off + a.nbytes <= cap:
-            np.frombuffer(shm.buf, dtype=np.uint8, count=a.nbytes, offset=base + off)[:] = a.reshape(-1)
-            out.append((a.shape[0], a.shape[1], off, None))
-            off += a.nbytes
-        else:
-            out.append((a.shape[0], a.shape[1], -1, a))
-    return out
+def _release_ring(ex, shm, addr, device):
+    ex.shutdown(wait=True, cancel_futures=True)
+    try:
+        import torch
+        torch.cuda.synchronize(device)  # the uploads out of the ring have run
+        torch._C._cudart.cudaHostUnregister(addr)
+    except Exception:  # (at interpreter exit the HIP runtime may already be gone)
+        pass
+    try:
+        shm.close()
+    except BufferError:  # a view still alive: the mapping goes with the process
+        pass
+    shm.unlink()
 
 
 class PinnedDecodeRing:
@@ -149,8 +126,12 @@ class PinnedDecodeRing:
         self.host = torch.frombuffer(self.shm.buf, dtype=torch.uint8)
         self._events = [None] * self.slots
         ctx = mp.get_context("forkserver")
-        ctx.set_forkserver_preload([__name__, "PIL.Image"])
+        ctx.set_forkserver_preload(["mmfd_decode_worker", "PIL.Image"])
         self._ex = cf.ProcessPoolExecutor(max_workers=self.workers, mp_context=ctx)
+        # (see DecodePool: the workers stop and the ring is released before the process exit joins
+        # its children)
+        self._fin = mp_util.Finalize(self, _release_ring, args=(self._ex, self.shm, self._addr, self.device),
+                                     exitpriority=10)
 
     def submit(self, paths, slot):
         ev = self._events[slot]
@@ -160,7 +141,7 @@ class PinnedDecodeRing:
         paths = list(paths)
         if len(paths) > self.gps * self.group:
             raise ValueError("batch larger than the ring slot")
-        return [self._ex.submit(_decode_group_into, self.shm.name, slot * self.sbytes + gi * self.gbytes, self.gbytes,
+        return [self._ex.submit(_dw.decode_group_into, self.shm.name, slot * self.sbytes + gi * self.gbytes, self.gbytes,
                                 paths[i:i + self.group])
                 for gi, i in enumerate(range(0, len(paths), self.group))]
 
@@ -201,19 +182,5 @@ class PinnedDecodeRing:
         return dsrc, shapes, offs
 
     def close(self):
-        import torch
-        if self._ex is None:
-            return
-        self._ex.shutdown(wait=True, cancel_futures=True)
-        self._ex = None
-        torch.cuda.synchronize(self.device)
-        torch._C._cudart.cudaHostUnregister(self._addr)
-        del self.host
-        self.shm.close()
-        self.shm.unlink()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        self.host = None  # (the view would pin the mapping)
+        self._fin()  # (runs once)
