@@ -688,6 +688,32 @@ __device__ __forceinline__ void cos_norm_q(uint4* f, float mult) {
 
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 
+// max / sum over the four lanes li, li+16, li+32, li+48 (the lane groups of one S^T column) by two
+// VALU half-swaps (v_permlane16/32_swap) instead of LDS permutes: the same pairs as __shfl_xor 16
+// then 32, so a sum rounds identically
+__device__ __forceinline__ float rows4_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// v2 kernel modes, chosen on the host: 0 = any (dropout, key bias, keep-bitmask, tested at run
+// time), 1 = plain (no dropout, no key bias: ViT, the fusion head at eval), 2 = hashed dropout with
+// a key bias and no bitmask (BERT training). The fixed modes take the per-subtile branches out of
+// the softmax loops, and mode 1 folds the scale into the exponent (exp2(s * c2 - m) as one fma).
+// bf16 forward only: the running max is raised only when some lane's chunk max passes it by more
+// than 8 (log2 units), so P = exp2(t - m) stays <= 256 and the O / l rescale (and its lane
+// broadcasts) is skipped for most chunks; O and l are scaled by the same stale max, so O / l is
+// unchanged up to rounding
+constexpr float V2_RESCALE_TH = 8.f;
+
 // per-key additive bias in log2 units for the head's batch row: log2e * key_bias (clamped so a
 // fully masked row stays finite, as HF's finfo.min mask does) for k < Lk, -inf for padded keys
 template <int NTH>
@@ -699,8 +725,10 @@ __device__ __forceinline__ void stage_kbias(float* dst, const AttnP& p, int64_t 
 // bf16 without the relative bias: at most 128 VGPRs (4 waves per SIMD) so that two 8-wave
 // workgroups share a CU — the bf16 K/V images allow it, and one VGPR over halves the occupancy
 // (ViT fwd +45 %); the REL instantiation needs ~148 and would spill under that bound
-template <typename T, int D, int HPB, bool REL>
+template <typename T, int D, int HPB, bool REL, int MODE>
 __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) attn_fwd_v2_kernel(AttnP p) {
+  static_assert(MODE == 0 || (HPB == 1 && !REL), "fixed modes: one head per workgroup, no relative bias");
+  constexpr bool LAZY = sizeof(T) == 2;
   // K/V of the head resident in LDS; each wave sweeps 16-query blocks with an online softmax (exp2
   // domain) over 64-key chunks (the last one holds only the padded key count's subtiles); key
   // mask/padding come from a per-key bias vector in LDS.
@@ -737,6 +765,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
   if (!active) return;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const bool drop = MODE == 0 ? p.p > 0.f : MODE == 2;
   const float c2 = p.scale * LOG2E;
   const float qmult = cosine ? expf(fminf(p.cos_ls[h], p.cos_max_log)) : 1.f;
   const bool rel4 = p.rel_bias && (p.Lk & 3) == 0 && (reinterpret_cast<uintptr_t>(p.rel_bias) & 15) == 0 &&
@@ -763,9 +792,11 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
     for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     // one 64-key chunk with NS 16-key subtiles present (NS < 4 only for the last, padded chunk;
     // NS = 0: that count at run time, `ns_rt`); a compile-time NS keeps every per-subtile branch
-    // out of the full chunks
-    auto chunk = [&](int k0, auto nsc, int ns_rt) {
+    // out of the full chunks. FOLD (mode 1, a full chunk of real keys): the chunk max is taken on
+    // the raw scores and the scale goes into the exponent's fma
+    auto chunk = [&](int k0, auto nsc, int ns_rt, auto foldc) {
       constexpr int NS = decltype(nsc)::value;
+      constexpr bool FOLD = decltype(foldc)::value;
       const int nsub = NS ? NS : ns_rt;
       const char* kc_img = k_img + k0 * C::RB;
       const char* vc_img = v_img + k0 * C::RB;
@@ -798,6 +829,13 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
         }
       }
       float mx = -INFINITY;
+      if constexpr (FOLD) {  // c2 > 0: max(s) * c2 == max(s * c2) (rounding is monotone)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[ks][r]);
+        mx *= c2;
+      } else {
 #pragma unroll
       for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
         if (ks >= nsub) continue;
@@ -824,21 +862,27 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
           mx = fmaxf(mx, t);
         }
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      }
+      mx = rows4_max(mx);
+      // (LAZY: a wave-uniform decision; otherwise every chunk rescales)
+      const bool grow = !LAZY || __ballot(mx > m + V2_RESCALE_TH) != 0ull;
+      float mnew = m, alpha = 1.f;
+      if (grow) {
+        mnew = fmaxf(m, mx);
+        alpha = __builtin_amdgcn_exp2f(m - mnew);
+      }
       float rs = 0.f;
 #pragma unroll
       for (int ks = 0; ks < (NS ? NS : 4); ++ks) {
         if (ks >= nsub) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(s[ks][r] - mnew);
+          const float e = FOLD ? __builtin_amdgcn_exp2f(fmaf(s[ks][r], c2, -mnew))
+                               : __builtin_amdgcn_exp2f(s[ks][r] - mnew);
           rs += e;
           s[ks][r] = e;
         }
-        if (p.p > 0.f) {  // one uniform branch per subtile
+        if (drop) {  // one uniform branch per subtile (none in the fixed modes)
           if (p.idx32) {
             const uint32_t c = rowc1 + (uint32_t)(k0 + ks * 16) * HASH_C1;
 #pragma unroll
@@ -853,7 +897,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
           }
         }
       }
-      if (p.p > 0.f && p.dm) {
+      if (MODE == 0 && p.p > 0.f && p.dm) {
         // the keep-bitmask for the backward, read back from P: a dropped element is 0, a kept one
         // e * keep_scale > 0 unless exp2 underflowed — and then the backward's P of it is 0 too,
         // so recording it as dropped changes no gradient (one register, no hash state kept live)
@@ -868,11 +912,13 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
       }
       lsum = lsum * alpha + rs;  // per-lane partial over this lane's keys; reduced at the end
       m = mnew;
+      if (grow) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ar = __shfl(alpha, 4 * g + r, 64);
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, 4 * g + r, 64);
 #pragma unroll
-        for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
+          for (int d = 0; d < C::DT; ++d) o[d][r] *= ar;
+        }
       }
 #pragma unroll
       for (int c = 0; c < (NS ? NS : 4) / SUBS; ++c) {
@@ -887,16 +933,19 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
     if constexpr (SUBS == 1) {
       // fp32 (MFMA-bound): one instance with the subtile count at run time — two compile-time
       // instances (full chunk + tail) raised it from 154 to 255 VGPRs and cost 7 % at L = 128
-      for (int k0 = 0; k0 < lk_pad; k0 += 64) chunk(k0, std::integral_constant<int, 0>{}, min(4, (lk_pad - k0) >> 4));
+      for (int k0 = 0; k0 < lk_pad; k0 += 64)
+        chunk(k0, std::integral_constant<int, 0>{}, min(4, (lk_pad - k0) >> 4), std::false_type{});
     } else {
       // bf16 (VALU-bound): the full chunks free of per-subtile branches (128 VGPRs: two workgroups
-      // per CU), the 32-key padded tail as its own instance
+      // per CU), the 32-key padded tail as its own instance; mode 1 folds the full chunks of real keys
       int k0 = 0;
-      for (; k0 + 64 <= lk_pad; k0 += 64) chunk(k0, std::integral_constant<int, 4>{}, 4);
-      if (k0 < lk_pad) chunk(k0, std::integral_constant<int, 2>{}, 2);
+      if constexpr (MODE == 1) {
+        for (; k0 + 64 <= p.Lk; k0 += 64) chunk(k0, std::integral_constant<int, 4>{}, 4, std::true_type{});
+      }
+      for (; k0 + 64 <= lk_pad; k0 += 64) chunk(k0, std::integral_constant<int, 4>{}, 4, std::false_type{});
+      if (k0 < lk_pad) chunk(k0, std::integral_constant<int, 2>{}, 2, std::false_type{});
     }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
+    lsum = rows4_sum(lsum);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float lr = __shfl(lsum, 4 * g + r, 64);
@@ -918,8 +967,9 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
   }
 }
 
-template <typename T, int D, int NTH, bool REL>
+template <typename T, int D, int NTH, bool REL, int MODE>
 __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
+  static_assert(MODE == 0 || !REL, "fixed modes: no relative bias");
   // Q/dO of the head resident in LDS (plus lse, delta in log2 units); each wave owns 16 keys.
   // REL: the additive [H][Lq][Lk] bias (MPNet / DeBERTa) — its loads and batch-modulus address
   // math stay out of the bias-free instantiation (BERT, ViT, fusion head)
@@ -940,7 +990,7 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   float* s_delta = s_lse + V2_LMAX;
   float* kbias = s_delta + V2_LMAX;
   uint32_t* s_dm = reinterpret_cast<uint32_t*>(kbias + V2_LMAX);  // dm_lds: the head's keep-bitmask rows
-  if (p.dm_lds) {
+  if (MODE == 0 && p.dm_lds) {
     const uint32_t* src = dm_row(p, bh, 0);
     const int nw = (int)p.Lq * p.dmw;
     for (int i = tid; i < lq_pad * p.dmw; i += NTH) s_dm[i] = i < nw ? src[i] : 0u;
@@ -963,6 +1013,7 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const bool drop = MODE == 0 ? p.p > 0.f : MODE == 2;
   const float c2 = p.scale * LOG2E;
   const int nkb = (int)((p.Lk + 15) / 16);
   const int nqc = lq_pad / KC;  // query chunks of one MFMA k-chunk
@@ -971,7 +1022,8 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
     uint4 kf[C::KCH], vf[C::KCH];
     load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
     load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
-    const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
+    // -inf for padded keys -> P = 0 (mode 1: their dK / dV rows are computed but never stored)
+    const float kb2 = MODE == 1 ? 0.f : kbias[mykey];
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
     const float* relcol = REL ? p.rel_bias + rb_off(p, b) + h * p.Lq * p.Lk + (mykey < p.Lk ? mykey : 0) : nullptr;
     f32x4 dkv[2 * C::DT];  // dV (even) and dK (odd) of each 16-wide D subtile
@@ -1021,8 +1073,8 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
         const float4 d4 = *reinterpret_cast<const float4*>(s_delta + qs * 16 + 4 * g);
         const float lq2[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
-        if (p.p > 0.f) {  // one uniform branch per subtile; the element index advances by Lk per query
-          if (p.dm_lds) {  // bit mykey of the query rows' words (LDS broadcast reads)
+        if (drop) {  // one uniform branch per subtile; the element index advances by Lk per query
+          if (MODE == 0 && p.dm_lds) {  // bit mykey of the query rows' words (LDS broadcast reads)
             const uint32_t* col = s_dm + (mykey >> 5);
             const int sh = (int)(mykey & 31);
 #pragma unroll
@@ -1042,9 +1094,14 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int lq = qs * 16 + 4 * g + r;
-          float t = fmaf(sv[r], c2, kb2);
-          if (REL && lq < p.Lq && mykey < p.Lk) t = fmaf(relcol[(int64_t)lq * p.Lk], LOG2E, t);
-          const float pr = __builtin_amdgcn_exp2f(t - lq2[r]);
+          float pr;
+          if constexpr (MODE == 1) {  // (lse = +inf on padded queries: P = 0)
+            pr = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -lq2[r]));
+          } else {
+            float t = fmaf(sv[r], c2, kb2);
+            if (REL && lq < p.Lq && mykey < p.Lk) t = fmaf(relcol[(int64_t)lq * p.Lk], LOG2E, t);
+            pr = __builtin_amdgcn_exp2f(t - lq2[r]);
+          }
           pd[h2][r] = pr * z[r];
           ds[h2][r] = pr * (dp[r] * z[r] - dl[r]);
         }
@@ -1082,8 +1139,9 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D, bool REL>
+template <typename T, int D, bool REL, int MODE>
 __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2_kernel(AttnP p) {
+  static_assert(MODE == 0 || !REL, "fixed modes: no relative bias");
   // K/V of the head resident in LDS; each wave owns 16 queries: dQ = dS K (REL as in dK/dV)
   using C = AT<T, D>;
   constexpr int KC = v2_kc<T>(), SUBS = KC / 16;
@@ -1109,6 +1167,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
   T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
+  const bool drop = MODE == 0 ? p.p > 0.f : MODE == 2;
   const float c2 = p.scale * LOG2E;
   const int nqb = (int)((p.Lq + 15) / 16);
   const int nkc = lk_pad / KC;
@@ -1134,7 +1193,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
     }
     const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
-    const uint32_t* dmrow = p.dm ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
+    const uint32_t* dmrow = MODE == 0 && p.dm ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
     f32x4 dq[C::DT];
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1153,7 +1212,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
     }
     for (int kc2 = 0; kc2 < nkc; ++kc2) {
       // the keep word of this chunk's keys (dropout bitmask), loaded ahead of the products
-      const uint32_t kw = (p.p > 0.f && p.dm) ? dmrow[(SUBS * kc2) >> 1] : 0u;
+      const uint32_t kw = (MODE == 0 && p.p > 0.f && p.dm) ? dmrow[(SUBS * kc2) >> 1] : 0u;
       uint4 tk[C::DT];  // transposed K fragments (B operand of dQ)
       if constexpr (PF) {
 #pragma unroll
@@ -1191,11 +1250,9 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
       for (int h2 = 0; h2 < SUBS; ++h2) {
         const int ks = SUBS * kc2 + h2;
         const f32x4 sv = sd[2 * h2], dp = sd[2 * h2 + 1];
-        const float4 kb4 = *reinterpret_cast<const float4*>(kbias + ks * 16 + 4 * g);
-        const float kbr[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
-        if (p.p > 0.f) {  // one uniform branch per subtile
-          if (p.dm) {
+        if (drop) {  // one uniform branch per subtile
+          if (MODE == 0 && p.dm) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) z[r] = ((kw >> ((ks & 1) * 16 + 4 * g + r)) & 1u) ? p.keep_scale : 0.f;
           } else if (p.idx32) {
@@ -1212,9 +1269,15 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = ks * 16 + 4 * g + r;
-          float t = fmaf(sv[r], c2, kbr[r]);
-          if (REL && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
-          const float pr = __builtin_amdgcn_exp2f(t - lse2);
+          float pr;
+          if constexpr (MODE == 1) {
+            // padded keys: their K rows are zero, so their dS adds nothing to dQ = dS K
+            pr = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -lse2));
+          } else {
+            float t = fmaf(sv[r], c2, kbias[ks * 16 + 4 * g + r]);
+            if (REL && key < p.Lk) t = fmaf(relrow[key], LOG2E, t);
+            pr = __builtin_amdgcn_exp2f(t - lse2);
+          }
           ds[h2][r] = pr * (dp[r] * z[r] - dlt);
         }
       }
@@ -1289,6 +1352,12 @@ __device__ uint64_t x6a_stamps[8192 * 8 * 16];
 constexpr int X6A_LMAX = 208;
 constexpr int X6A_RB = 128;  // bytes per plane row (64 bf16)
 constexpr int X6A_LDS = 6 * X6A_LMAX * X6A_RB + 3 * X6A_LMAX * 4;
+
+// A/B switch: MMFD_ATTN_V2_GENERIC=1 (or mmfd_debug_set_attn_v2_generic) runs every v2 call on mode 0
+int g_v2_generic = [] {
+  const char* v = getenv("MMFD_ATTN_V2_GENERIC");
+  return v && atoi(v) != 0 ? 1 : 0;
+}();
 
 int g_fp32_attn_mode = [] {
   const char* v = getenv("MMFD_FP32_ATTN");
@@ -2237,28 +2306,43 @@ __global__ void dm_fill_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D, int HPB, bool REL>
+template <typename T, int D, int HPB, bool REL, int MODE>
 void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
   constexpr int RB = AT<T, D>::RB;
   const int lk_pad = v2_pad(p.Lk, v2_kc<T>());
   const int lds = HPB * (2 * lk_pad * RB + lk_pad * 4);
   constexpr int lmax = HPB == 1 ? (sizeof(T) == 2 ? V2_LMAX_FWD : V2_LMAX) : 64;
-  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<T, D, HPB, REL>),
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_fwd_v2_kernel<T, D, HPB, REL, MODE>),
                                    HPB * (2 * lmax * RB + lmax * 4)), true);
   (void)once;
   const int64_t nbh = p.B * p.H;
-  hipLaunchKernelGGL((attn_fwd_v2_kernel<T, D, HPB, REL>), dim3((unsigned)((nbh + HPB - 1) / HPB)), dim3(V2_THREADS),
-                     lds, s, p);
+  hipLaunchKernelGGL((attn_fwd_v2_kernel<T, D, HPB, REL, MODE>), dim3((unsigned)((nbh + HPB - 1) / HPB)),
+                     dim3(V2_THREADS), lds, s, p);
+}
+
+// the fixed v2 mode for these arguments (see V2_RESCALE_TH): 1 plain, 2 hashed dropout + key bias,
+// 0 anything else (relative bias, keep-bitmask, dropout without a key bias, ...)
+inline int v2_mode(const AttnP& p) {
+  if (p.rel_bias || g_v2_generic) return 0;
+  if (p.p == 0.f && !p.key_bias) return 1;
+  if (p.p > 0.f && p.key_bias && !p.dm) return 2;
+  return 0;
 }
 
 // the relative-bias instantiation carries the extra loads / registers; plain attention (BERT, ViT,
 // fusion head) keeps the bias-free one
 template <typename T, int D, int HPB>
 void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
-  if (p.rel_bias)
-    launch_fwd_v2_hpb<T, D, HPB, true>(p, s);
-  else
-    launch_fwd_v2_hpb<T, D, HPB, false>(p, s);
+  if (p.rel_bias) {
+    launch_fwd_v2_hpb<T, D, HPB, true, 0>(p, s);
+  } else if constexpr (HPB == 1) {
+    const int mode = v2_mode(p);
+    if (mode == 1) launch_fwd_v2_hpb<T, D, 1, false, 1>(p, s);
+    else if (mode == 2) launch_fwd_v2_hpb<T, D, 1, false, 2>(p, s);
+    else launch_fwd_v2_hpb<T, D, 1, false, 0>(p, s);
+  } else {
+    launch_fwd_v2_hpb<T, D, HPB, false, 0>(p, s);
+  }
 }
 
 template <typename T, int D>
@@ -2272,7 +2356,7 @@ void launch_fwd_v2(const AttnP& p, hipStream_t s) {
     launch_fwd_v2_hpb<T, D, 1>(p, s);
 }
 
-template <typename T, int D, bool REL>
+template <typename T, int D, bool REL, int MODE>
 void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
   constexpr int RB = AT<T, D>::RB, NTH = V2T<T>::DKDV_THREADS;
   const int lq_pad = v2_pad(p.Lq, v2_kc<T>()), lk_pad = v2_pad(p.Lk, v2_kc<T>());
@@ -2284,22 +2368,23 @@ void launch_bwd_v2_rel(const AttnP& p, hipStream_t s) {
   AttnP q = p;  // dK/dV stages the head's keep-bitmask rows in LDS when the caller kept them
   q.dm_lds = p.p > 0.f && p.dm && lds1n + lq_pad * p.dmw * 4 <= lds1_max;
   const int lds1 = lds1n + (q.dm_lds ? lq_pad * p.dmw * 4 : 0);
-  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH, REL>), lds1_max),
-                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D, REL>),
+  static bool once = (set_lds_attr(reinterpret_cast<const void*>(&attn_dkdv_v2_kernel<T, D, NTH, REL, MODE>), lds1_max),
+                      set_lds_attr(reinterpret_cast<const void*>(&attn_dq_v2_kernel<T, D, REL, MODE>),
                                    NI2 * V2_LMAX * RB + V2_LMAX * 4),
                       true);
   (void)once;
   // dQ first: it writes delta = rowsum(dO * O) for dK/dV (no separate delta pass)
-  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, q);
-  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, q);
+  hipLaunchKernelGGL((attn_dq_v2_kernel<T, D, REL, MODE>), dim3((unsigned)(p.B * p.H)), dim3(V2_THREADS), lds2, s, q);
+  hipLaunchKernelGGL((attn_dkdv_v2_kernel<T, D, NTH, REL, MODE>), dim3((unsigned)(p.B * p.H)), dim3(NTH), lds1, s, q);
 }
 
 template <typename T, int D>
 void launch_bwd_v2(const AttnP& p, hipStream_t s) {
-  if (p.rel_bias)
-    launch_bwd_v2_rel<T, D, true>(p, s);
-  else
-    launch_bwd_v2_rel<T, D, false>(p, s);
+  const int mode = v2_mode(p);
+  if (p.rel_bias) launch_bwd_v2_rel<T, D, true, 0>(p, s);
+  else if (mode == 1) launch_bwd_v2_rel<T, D, false, 1>(p, s);
+  else if (mode == 2) launch_bwd_v2_rel<T, D, false, 2>(p, s);
+  else launch_bwd_v2_rel<T, D, false, 0>(p, s);
 }
 
 template <typename T, int D>
@@ -2395,6 +2480,13 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (a->dqkv_planes && !v2)  // the v1 kernels write fp32 only: split afterwards
     return mmfd_split3(p.B * p.Lq, W, (const float*)a->dq, W, a->dqkv_planes, stream);
   return 0;
+}
+
+// A/B switch for the fixed v2 modes (not part of include/mmfd.h): returns the old value
+extern "C" int mmfd_debug_set_attn_v2_generic(int on) {
+  const int old = g_v2_generic;
+  g_v2_generic = on ? 1 : 0;
+  return old;
 }
 
 extern "C" int mmfd_set_fp32_attn_mode(int mode) {

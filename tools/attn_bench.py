@@ -1,7 +1,8 @@
 """Attention kernels at the encoder shapes (bs=256 pairs -> 512 sequences x 12 heads, D=64):
 BERT L=128 with key mask + dropout 0.1, ViT L=197 without. Prints per-kernel-call times.
 BERT runs twice: the backward re-hashing the dropout mask, and reading the forward's keep-bitmask.
-python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native] [--planes]"""
+--ab-generic: every case also on the v2 kernels' generic mode 0 (mmfd_debug_set_attn_v2_generic)
+python tools/attn_bench.py [--iters N] [--only bert|vit] [--fp32-mode split|native] [--planes] [--ab-generic]"""
 import argparse
 import os
 import sys
@@ -68,9 +69,16 @@ if __name__ == "__main__":
     ap.add_argument("--fp32-mode", default="split", help="fp32 attention: split (bf16 planes) or native")
     ap.add_argument("--planes", action="store_true", help="fp32: output / gradient planes as the encoders use them")
     ap.add_argument("--bert-p", type=float, default=0.1, help="BERT case dropout probability")
+    ap.add_argument("--ab-generic", action="store_true")
     a = ap.parse_args()
     K.set_fp32_attn_mode(a.fp32_mode)
-    for dt in a.dtype.split(","):
+    import ctypes
+    gen = K.lib().mmfd_debug_set_attn_v2_generic
+    gen.argtypes, gen.restype = [ctypes.c_int], ctypes.c_int
+    for dt, g in [(d, x) for d in a.dtype.split(",") for x in ((1, 0) if a.ab_generic else (0,))]:
+        gen(g)
+        if a.ab_generic:
+            print(f"-- v2 {'generic mode 0' if g else 'fixed modes'}", flush=True)
         t = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt]
         if a.only in ("", "bert"):
             case(f"{dt} bert L=128 mask p={a.bert_p} hash   ", 128, True, a.bert_p, a.iters, t, a.planes)
