@@ -266,6 +266,12 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     // kept in registers. Refills: X(t) issues A-h1 of
     // t+1 (last read in Y(t-1)), Y(t) issues A-h0 / B-h0 / B-h1 of t+2 (last read in X(t)); each
     // phase then waits until at most the 8 pieces issued after the next phase's operands remain.
+    // Segment stamps of one mid-loop K-tile (G8_PSTAMP, tools/g8_stamps.py): each phase's read
+    // side (fragment reads ~30 cycles per ds_read_b128 issue, LDS-DMA pieces ~130 cycles each,
+    // the vmcnt wait < 100) outlasts the partner row's 32 MFMAs, so a K-tile takes ~3,600 cycles
+    // against 2,048 of MFMA. Moving two of Y's six pieces into X (four per phase) measured
+    // neutral (+0.5 % over the encoder shapes, profiles/r04_bf16_g8_stamps.log): a piece costs
+    // more beside X's 16 reads than beside Y's 8.
     uint4 fbh[2][2];
     for (int t = 0; t < nk; ++t) {
       bool rs_t = false;
@@ -274,31 +280,44 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         rs_ph = rs_ph + 1 == rs_cols ? 0 : rs_ph + 1;
       }
       // phase X(t)
+      G8_PSTAMP(8);
       g8_frag_a<T, TA>(fa, img(t, 0), wr, lane);
       g8_frag_b<T, TB>(fb, img(t, 2), wc, lane);
       g8_frag_b<T, TB>(fbh, img(t, 3), wc, lane);
       if (rs_t) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      G8_PSTAMP(17);
       if (t + 1 < nk) {
         issue(1, t + 1);
+        G8_PSTAMP(18);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      G8_PSTAMP(9);
       g8_pre_barrier();
+      G8_PSTAMP(10);
       g8_mma2<T>(acc[0][0], acc[0][1], fa, fb, fbh);
+      G8_PSTAMP(11);
       g8_barrier();
       // phase Y(t)
+      G8_PSTAMP(12);
       g8_frag_a<T, TA>(fa, img(t, 1), wr, lane);
       if (rs_t) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      G8_PSTAMP(19);
       if (t + 2 < nk) {
         issue(0, t + 2); issue(2, t + 2); issue(3, t + 2);
+        G8_PSTAMP(20);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      G8_PSTAMP(13);
       g8_pre_barrier();
+      G8_PSTAMP(14);
       g8_mma2<T>(acc[1][0], acc[1][1], fa, fb, fbh);
+      G8_PSTAMP(15);
       g8_barrier();
+      G8_PSTAMP(16);
     }
   } else {
     // fp32: four phases of one quadrant each (the two-phase schedule pushes the fp32 layout-1

@@ -463,7 +463,7 @@ __device__ __forceinline__ float g8_rowsum(const char* img, int wr, int wc, int 
 // Diagnostic build only (-DMMFD_G8_STAMPS, tools/g8_stamps.py): per-wave s_memtime stamps at
 // the phase boundaries of the 256x256 kernel, to a buffer no computation reads.
 #ifdef MMFD_G8_STAMPS
-constexpr int G8_NSTAMP = 8;
+constexpr int G8_NSTAMP = 24;  // 0-7 kernel phases, 8-16 the bf16 main-loop segments of K-tile 4
 __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
 #define G8_STAMP(k)                                                                                    \
   do {                                                                                                 \
@@ -471,8 +471,13 @@ __device__ uint64_t g8_stamps[16384 * 8 * G8_NSTAMP];
     const int64_t b__ = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;                                 \
     if (lane == 0 && b__ < 16384) g8_stamps[(b__ * 8 + wave) * G8_NSTAMP + (k)] = t__;                \
   } while (0)
+#define G8_PSTAMP(k)                                                                                   \
+  do {                                                                                                 \
+    if (t == 4) G8_STAMP(k);                                                                           \
+  } while (0)
 #else
 #define G8_STAMP(k) do { } while (0)
+#define G8_PSTAMP(k) do { } while (0)
 #endif
 
 // Split-operand LDS slots (gemm_x6f.hip): one plane of one 128-row / 128-column half-tile of a

@@ -2,7 +2,10 @@
 -DMMFD_G8_STAMPS build of libmmfd_hip under tools/_stamps/; the product library is untouched).
 Stamps: 0 start, 1 mainloop done, 2 after the re-align + vmcnt(0) + barrier, 3 staging written,
 4 after the staging barrier, 5 first 128 rows read back + stored, 6 epilogue issued, 7 stores
-retired (vmcnt(0)).   python tools/g8_stamps.py [M N K [plain|gelu|gelubwd] [bf16|fp32]]"""
+retired (vmcnt(0)); bf16 main-loop segments of K-tile 4 (stamps 8-16): X reads + refill issue +
+vmcnt, X pre-barrier, X MFMAs, X barrier, then the same for Y.
+Stamps 17-20 split each read side into fragment reads / refill issue / vmcnt wait.
+python tools/g8_stamps.py [M N K [plain|gelu|gelubwd] [bf16|fp32]]"""
 import ctypes
 import os
 import subprocess
@@ -52,9 +55,11 @@ for _ in range(5):
         K.gemm(A, B, out=out)
 torch.cuda.synchronize()
 nblk = min((M // 256) * (N // 256), 16384)
-buf = np.zeros(16384 * 8 * 8, np.uint64)
+NS = 24
+buf = np.zeros(16384 * 8 * NS, np.uint64)
 assert lib.mmfd_debug_g8_stamps(buf.ctypes.data, buf.nbytes) == 0
-st = buf.reshape(16384, 8, 8)[:nblk].astype(np.int64)
+full = buf.reshape(16384, 8, NS)[:nblk].astype(np.int64)
+st = full[:, :, :8]
 d = np.diff(st, axis=2)  # [blocks, waves, 7]
 names = ["mainloop", "realign+vmcnt+barrier", "stage writes", "stage barrier", "rows 0-127 epilogue",
          "rows 128-255 epilogue", "store drain"]
@@ -64,3 +69,18 @@ for i, n in enumerate(names):
     print(f"  {n:24s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
 tot = st[:, :, 7] - st[:, :, 0]
 print(f"  {'total':24s} {np.median(tot):9.0f} {np.percentile(tot, 90):9.0f}")
+if dt == torch.bfloat16 and Kd >= 5 * 64:
+    seg = np.diff(full[:, :, 8:17], axis=2)
+    sn = ["X reads+issue+wait", "X pre-barrier", "X MFMAs", "X barrier", "Y reads+issue+wait", "Y pre-barrier",
+          "Y MFMAs", "Y barrier"]
+    print("K-tile 4 segments (median / p90 over waves):")
+    for i, n in enumerate(sn):
+        v = seg[:, :, i].ravel()
+        print(f"  {n:24s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
+    if True:  # the reads / issue / wait split
+        for n, a, b in (("X reads", 8, 17), ("X refill issue", 17, 18), ("X vmcnt wait", 18, 9),
+                        ("Y reads", 12, 19), ("Y refill issue", 19, 20), ("Y vmcnt wait", 20, 13)):
+            v = (full[:, :, b] - full[:, :, a]).ravel()
+            print(f"  {n:24s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
+    kt = full[:, :, 16] - full[:, :, 8]
+    print(f"  {'K-tile':24s} {np.median(kt):9.0f} {np.percentile(kt, 90):9.0f}")
