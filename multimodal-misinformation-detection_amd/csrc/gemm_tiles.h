@@ -61,6 +61,8 @@ template <typename T> struct GT {
 
 
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
 __device__ __forceinline__ void split1(float x, bf16& h, bf16& m, bf16& l) {
   h = (bf16)x;
   const float r = x - (float)h;
@@ -122,9 +124,12 @@ template <> struct V8<bf16> {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
   }
+  // streaming (nontemporal) stores: the epilogue's outputs are written once and read by a later
+  // launch; +1.3 % over the bf16 encoder GEMM shapes, +0.6 % on the bf16 step (same-box A/B,
+  // tools/lib_ab.sh, profiles/r04_epi_nt_ab.log)
   __device__ __forceinline__ static void store(bf16* p, const float (&v)[8]) {
     bf16x8 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
-    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, o);
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, o), reinterpret_cast<u32x4_t*>(p));
   }
 };
 template <> struct V8<float> {
@@ -133,6 +138,8 @@ template <> struct V8<float> {
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   }
   __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    // (nontemporal here and in planes_store8 measured neutral on the fp32 GEMMs and −0.3 % on the
+    // fp32 step: profiles/r04_epi_nt_ab.log)
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
