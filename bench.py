@@ -886,6 +886,14 @@ def train_leg(args, dev, world, rank, precision):
             log(f"rank {rank}: DP step capture failed ({e!r}); eager steps")
             tr.release_graph()
             graphed = False
+    if world > 1 and not args.no_graph and os.environ.get("MMFD_DP_GRAPH", "1") == "1":
+        # every rank runs the same kind of step: if any rank's capture failed, all go eager
+        ok = torch.tensor([1 if graphed else 0], device=dev, dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if graphed and int(ok.item()) == 0:
+            log(f"rank {rank}: another rank's capture failed; eager steps")
+            tr.release_graph()
+            graphed = False
     if graphed:
         for _ in range(args.warmup):
             tr.replay()
