@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import logging
 import os
+import time
 
 import numpy as np
 import torch
@@ -230,6 +231,14 @@ class FusionTrainer:
             for _ in range(warmup):  # optimizer state, weight shadows, kernel attributes
                 self.step(batch)
         torch.cuda.current_stream().wait_stream(s)
+        if self.dp is not None and self.dp._active():
+            # ProcessGroupNCCL's watchdog thread polls the eager warm-up's collectives (their events
+            # on RCCL's stream) every ~100 ms; RCCL's stream joins the capture with the first
+            # captured all-reduce, and a poll that lands inside the capture aborts the process
+            # (hipErrorCapturedEvent / hipErrorStreamCaptureUnsupported, 2 of 4 world-1 runs): let
+            # the watchdog retire every eager collective before capturing
+            torch.cuda.synchronize()
+            time.sleep(float(os.environ.get("MMFD_DP_QUIESCE_S", "0.5")))
         self.optimizer.prepare_capture()  # pointer tables outside the graph's memory pool
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

@@ -22,6 +22,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
+# bounded worker waits (tests/mp_util.py)
+from tests.mp_util import collect as _collect  # noqa: E402
+from tests.mp_util import watchdog as _watchdog  # noqa: E402
+
+
 def _grads(tr):
     out = {}
     for pre, m in (("bert.", tr.text_encoder), ("vit.", tr.image_encoder), ("head.", tr.head)):
@@ -42,6 +47,7 @@ def _half(batch, rank, world):
 
 def _worker(rank, world, port, q):
     import torch.distributed as dist
+    _watchdog()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -76,12 +82,9 @@ def test_dp_two_ranks_match_full_batch():
     for p in procs:
         p.start()
     res, params = {}, {}
-    for _ in range(world):
-        r, g1, pr = q.get(timeout=300)
+    for r, g1, pr in _collect(procs, q, world):
         res[r], params[r] = g1, pr
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    assert all(p.exitcode == 0 for p in procs)
     for k in params[0]:  # replicas started from different seeds, trained 2 steps: identical
         assert (params[0][k] == params[1][k]).all(), k
     tr, _ = build_pair("fp32", dropout=0.0)
@@ -101,6 +104,7 @@ def test_dp_two_ranks_match_full_batch():
 # ---- full size: bert-base + ViT-B/16 + head, default 32 MB buckets, two encoder streams ----------
 def _worker_full(rank, world, port, q):
     import torch.distributed as dist
+    _watchdog()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -139,13 +143,10 @@ def test_dp_full_size_default_buckets_two_streams():
     for p in procs:
         p.start()
     res, nb = {}, {}
-    for _ in range(world):
-        r, g1, buckets = q.get(timeout=500)
+    for r, g1, buckets in _collect(procs, q, world):
         assert buckets is not None, g1  # the worker's traceback
         res[r], nb[r] = g1, buckets
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    assert all(p.exitcode == 0 for p in procs)
     print(f"buckets per stream: {nb[0]}", flush=True)
     assert len(nb[0]) == 2 and sum(nb[0].values()) >= 20, nb[0]  # buckets on both streams
     tr = build_flagship("cuda", "fp32", dropout=0.0, seed=42, encoder_dropout=0.0)
@@ -168,6 +169,7 @@ def test_dp_full_size_default_buckets_two_streams():
 # ---- RCCL: ProcessGroupNCCL with one rank, the overlapped all-reduce forced on ----------------------
 def _worker_nccl(port, q):
     import torch.distributed as dist
+    _watchdog()
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
@@ -230,8 +232,7 @@ def test_dp_nccl_world1_overlapped_allreduce():
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
     p.start()
-    out = q.get(timeout=500)
-    p.join(timeout=120)
+    out = _collect([p], q, 1)[0]
     assert "error" not in out, out.get("error")
     assert p.exitcode == 0
     assert out.pop("backend") == "nccl"
@@ -244,6 +245,7 @@ def _worker_nccl_graph(port, q):
     """world-1 RCCL: a DP trainer whose whole step (with the bucketed all-reduce) is captured in a
     HIP graph vs the plain captured trainer, two replays on two batches each"""
     import torch.distributed as dist
+    _watchdog()
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
@@ -306,8 +308,7 @@ def test_dp_nccl_world1_graph_captured_step():
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl_graph, args=(_free_port(), q))
     p.start()
-    out = q.get(timeout=500)
-    p.join(timeout=120)
+    out = _collect([p], q, 1)[0]
     assert "error" not in out, out.get("error")
     assert p.exitcode == 0
     for name, (steps, nb) in out.items():

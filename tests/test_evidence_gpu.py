@@ -255,6 +255,8 @@ def _extractors():
 
 def _corpus_worker(rank, world, port, d, q):
     import torch.distributed as dist
+    from tests.mp_util import watchdog
+    watchdog(240)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -296,12 +298,10 @@ def test_sharded_corpus_build_hip_equals_single_process(tmp_path):
     procs = [ctx.Process(target=_corpus_worker, args=(r, world, port, d, q)) for r in range(world)]
     for p in procs:
         p.start()
-    for _ in range(world):
-        r, err = q.get(timeout=400)
+    from tests.mp_util import collect
+    for r, err in collect(procs, q, world, deadline=260):
         assert err is None, err
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    assert all(p.exitcode == 0 for p in procs)
     merged = load_corpus_pickle(os.path.join(d, "sharded.pkl"))
     assert list(merged) == list(single.feature_dict)
     for k in merged:

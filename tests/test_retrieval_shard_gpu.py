@@ -28,6 +28,8 @@ def _data():
 
 def _worker(rank, world, port, q):
     import torch.distributed as dist
+    from tests.mp_util import watchdog
+    watchdog()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -50,13 +52,11 @@ def test_sharded_search_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
+    from tests.mp_util import collect
     out = {}
-    for _ in range(world):
-        r, hits, v, i = q.get(timeout=300)
+    for r, hits, v, i in collect(procs, q, world):
         out[r] = (hits, v, i)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    assert all(p.exitcode == 0 for p in procs)
     feats, queries = _data()
     ref = CorpusIndex(feats, mode="pair", eps=1e-6, device="cuda")
     ref_hits = ref.search(queries.cuda(), 12)
