@@ -624,16 +624,64 @@ template <typename T, int D> struct V2 { static constexpr bool DUAL = sizeof(T) 
 template <typename T> __host__ __device__ constexpr int v2_kc() { return sizeof(T) == 2 ? 32 : 16; }
 __host__ __device__ inline int v2_pad(int64_t n, int kc) { return (int)((n + kc - 1) / kc * kc); }
 
+// Head staging: STAGE_BATCH 16-B chunks per thread and source are loaded before the first LDS
+// write, so a workgroup waits out one global-load latency per batch instead of one per chunk (the
+// one-chunk loop waited vmcnt(0) before every ds_write: 14 serial round trips for a ViT dK/dV head)
+constexpr int STAGE_BATCH = 4;
+
+template <typename T, int D, bool TR>
+__device__ __forceinline__ int stage_off(int r, int ch) {
+  return TR ? (r * AT<T, D>::RB + (tr_chunk<T, D>(r, ch) << 4)) : row_off<T, D>(r, ch);
+}
+
 template <typename T, int D, bool TR, int NTH = V2_THREADS>
 __device__ __forceinline__ void stage_all(char* lds, const T* __restrict__ base, int64_t st, int64_t nrows,
                                           int nrows_pad, int tid, int dreal) {
   constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
-  for (int c = tid; c < nrows_pad * NCH; c += NTH) {
-    const int r = c / NCH, ch = c % NCH;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < nrows && ch * EPC < dreal) v = *reinterpret_cast<const uint4*>(base + (int64_t)r * st + ch * EPC);
-    const int off = TR ? (r * AT<T, D>::RB + (tr_chunk<T, D>(r, ch) << 4)) : row_off<T, D>(r, ch);
-    *reinterpret_cast<uint4*>(lds + off) = v;
+  const int total = nrows_pad * NCH;
+  for (int c0 = tid; c0 < total; c0 += NTH * STAGE_BATCH) {
+    uint4 v[STAGE_BATCH];
+#pragma unroll
+    for (int j = 0; j < STAGE_BATCH; ++j) {
+      const int c = c0 + j * NTH, r = c / NCH, ch = c % NCH;
+      v[j] = make_uint4(0, 0, 0, 0);
+      if (c < total && r < nrows && ch * EPC < dreal) v[j] = *reinterpret_cast<const uint4*>(base + (int64_t)r * st + ch * EPC);
+    }
+#pragma unroll
+    for (int j = 0; j < STAGE_BATCH; ++j) {
+      const int c = c0 + j * NTH;
+      if (c < total) *reinterpret_cast<uint4*>(lds + stage_off<T, D, TR>(c / NCH, c % NCH)) = v[j];
+    }
+  }
+}
+
+// two head slices of the same row count (K and V, Q and dO, or one tensor into both layouts),
+// every load of a batch of both issued before its writes
+template <typename T, int D, bool TRA, bool TRB, int NTH = V2_THREADS>
+__device__ __forceinline__ void stage_two(char* lds_a, const T* __restrict__ base_a, int64_t st_a, char* lds_b,
+                                          const T* __restrict__ base_b, int64_t st_b, int64_t nrows, int nrows_pad,
+                                          int tid, int dreal) {
+  constexpr int NCH = AT<T, D>::NCH, EPC = AT<T, D>::EPC;
+  const int total = nrows_pad * NCH;
+  for (int c0 = tid; c0 < total; c0 += NTH * STAGE_BATCH) {
+    uint4 va[STAGE_BATCH], vb[STAGE_BATCH];
+#pragma unroll
+    for (int j = 0; j < STAGE_BATCH; ++j) {
+      const int c = c0 + j * NTH, r = c / NCH, ch = c % NCH;
+      va[j] = vb[j] = make_uint4(0, 0, 0, 0);
+      if (c < total && r < nrows && ch * EPC < dreal) {
+        va[j] = *reinterpret_cast<const uint4*>(base_a + (int64_t)r * st_a + ch * EPC);
+        vb[j] = *reinterpret_cast<const uint4*>(base_b + (int64_t)r * st_b + ch * EPC);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < STAGE_BATCH; ++j) {
+      const int c = c0 + j * NTH, r = c / NCH, ch = c % NCH;
+      if (c < total) {
+        *reinterpret_cast<uint4*>(lds_a + stage_off<T, D, TRA>(r, ch)) = va[j];
+        *reinterpret_cast<uint4*>(lds_b + stage_off<T, D, TRB>(r, ch)) = vb[j];
+      }
+    }
   }
 }
 
@@ -753,13 +801,19 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
   float* kbias = reinterpret_cast<float*>(hbase + 2 * lk_pad * C::RB);
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* kb_g = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const int nqb = (int)((p.Lq + 15) / 16);
+  uint4 qn[C::KCH];  // next query block's fragments, prefetched one block ahead (the first under the staging)
+  load_row_regs<T, D>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
   bool cosine = false;
   if constexpr (sizeof(T) == 2) {
     cosine = REL && p.cos_ls != nullptr;
     if (cosine) stage_rows_cos<D, TPH>(k_img, kb_g, p.k_st, p.Lk, lk_pad, htid, p.D);
   }
-  if (!cosine) stage_all<T, D, false, TPH>(k_img, kb_g, p.k_st, p.Lk, lk_pad, htid, p.D);
-  stage_all<T, D, true, TPH>(v_img, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, htid, p.D);
+  const T* vb_g = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
+  if (!cosine)
+    stage_two<T, D, false, true, TPH>(k_img, kb_g, p.k_st, v_img, vb_g, p.v_st, p.Lk, lk_pad, htid, p.D);
+  else
+    stage_all<T, D, true, TPH>(v_img, vb_g, p.v_st, p.Lk, lk_pad, htid, p.D);
   stage_kbias<TPH>(kbias, p, b, lk_pad, htid);
   __syncthreads();
   if (!active) return;
@@ -771,9 +825,6 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
   const bool rel4 = p.rel_bias && (p.Lk & 3) == 0 && (reinterpret_cast<uintptr_t>(p.rel_bias) & 15) == 0 &&
                     (p.rb_sb & 3) == 0;
   T* ob = reinterpret_cast<T*>(p.o) + b * p.o_sb + h * p.D;
-  const int nqb = (int)((p.Lq + 15) / 16);
-  uint4 qn[C::KCH];  // next query block's fragments, prefetched one block ahead
-  load_row_regs<T, D>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
   for (int qbk = wave; qbk < nqb; qbk += WPH) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
     uint4 qf[C::KCH];
@@ -997,18 +1048,24 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   }
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
-  stage_all<T, D, false, NTH>(q_row, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  if (!DUAL) stage_all<T, D, true, NTH>(q_tr, qb, p.q_st, p.Lq, lq_pad, tid, p.D);
-  stage_all<T, D, false, NTH>(do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
-  if (!DUAL) stage_all<T, D, true, NTH>(do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
+  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
+  // PF (bf16 fixed modes, where the registers allow it): the wave's next key block loaded one block
+  // ahead, the first under the staging
+  constexpr bool PF = sizeof(T) == 2 && !REL && MODE != 0;
+  uint4 kn[C::KCH], vn[C::KCH];
+  if constexpr (PF) {
+    load_row_regs<T, D>(kn, kb, p.k_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
+    load_row_regs<T, D>(vn, vb, p.v_st, (int64_t)wave * 16 + li, p.Lk, lane, p.D);
+  }
+  stage_two<T, D, false, false, NTH>(q_row, qb, p.q_st, do_row, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
+  if (!DUAL) stage_two<T, D, true, true, NTH>(q_tr, qb, p.q_st, do_tr, dob, p.do_st, p.Lq, lq_pad, tid, p.D);
   for (int i = tid; i < lq_pad; i += NTH) {
     s_lse[i] = i < p.Lq ? p.lse[bh * p.Lq + i] * LOG2E : INFINITY;
     s_delta[i] = i < p.Lq ? p.delta[bh * p.Lq + i] : 0.f;
   }
   stage_kbias<NTH>(kbias, p, b, (int)((p.Lk + 15) & ~15), tid);
   __syncthreads();
-  const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
-  const T* vb = reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D;
   T* dkb = reinterpret_cast<T*>(p.dk) + b * p.dk_sb + h * p.D;
   T* dvb = reinterpret_cast<T*>(p.dv) + b * p.dv_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
@@ -1020,8 +1077,15 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
   for (int kbk = wave; kbk < nkb; kbk += NTH / 64) {
     const int64_t k0 = (int64_t)kbk * 16, mykey = k0 + li;
     uint4 kf[C::KCH], vf[C::KCH];
-    load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
-    load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    if constexpr (PF) {
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) { kf[kc] = kn[kc]; vf[kc] = vn[kc]; }
+      load_row_regs<T, D>(kn, kb, p.k_st, k0 + NTH / 64 * 16 + li, p.Lk, lane, p.D);
+      load_row_regs<T, D>(vn, vb, p.v_st, k0 + NTH / 64 * 16 + li, p.Lk, lane, p.D);
+    } else {
+      load_row_regs<T, D>(kf, kb, p.k_st, mykey, p.Lk, lane, p.D);
+      load_row_regs<T, D>(vf, vb, p.v_st, mykey, p.Lk, lane, p.D);
+    }
     // -inf for padded keys -> P = 0 (mode 1: their dK / dV rows are computed but never stored)
     const float kb2 = MODE == 1 ? 0.f : kbias[mykey];
     const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
@@ -1157,13 +1221,23 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
   char* k_tr = DUAL ? k_row : smem + 2 * img;
   float* kbias = reinterpret_cast<float*>(smem + (DUAL ? 2 : 3) * img);
   const T* kb = reinterpret_cast<const T*>(p.k) + b * p.k_sb + h * p.D;
-  stage_all<T, D, false>(k_row, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
-  if (!DUAL) stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
-  stage_all<T, D, false>(v_row, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D, p.v_st, p.Lk, lk_pad, tid, p.D);
-  stage_kbias<V2_THREADS>(kbias, p, b, lk_pad, tid);
-  __syncthreads();
   const T* qb = reinterpret_cast<const T*>(p.q) + b * p.q_sb + h * p.D;
   const T* dob = reinterpret_cast<const T*>(p.dout) + b * p.do_sb + h * p.D;
+  const T* obq = reinterpret_cast<const T*>(p.o) + b * p.o_sb + h * p.D;
+  // PF (bf16 fixed modes, where the registers allow it): the wave's next query block's Q / dO / O
+  // rows loaded one block ahead, the first under the staging
+  constexpr bool PF = sizeof(T) == 2 && !REL && MODE != 0;
+  uint4 qn[C::KCH], dn[C::KCH], on[C::KCH];
+  if constexpr (PF) {
+    load_row_regs<T, D>(qn, qb, p.q_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+    load_row_regs<T, D>(dn, dob, p.do_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+    load_row_regs<T, D>(on, obq, p.o_st, (int64_t)wave * 16 + li, p.Lq, lane, p.D);
+  }
+  stage_two<T, D, false, false>(k_row, kb, p.k_st, v_row, reinterpret_cast<const T*>(p.v) + b * p.v_sb + h * p.D,
+                                p.v_st, p.Lk, lk_pad, tid, p.D);
+  if (!DUAL) stage_all<T, D, true>(k_tr, kb, p.k_st, p.Lk, lk_pad, tid, p.D);
+  stage_kbias<V2_THREADS>(kbias, p, b, lk_pad, tid);
+  __syncthreads();
   T* dqb = reinterpret_cast<T*>(p.dq) + b * p.dq_sb + h * p.D;
   const uint64_t seed = p.p > 0.f ? *p.seed : 0ull;
   const uint32_t hkey = mmfd_hash_key(seed, p.salt);
@@ -1173,16 +1247,26 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
   const int nkc = lk_pad / KC;
   for (int qbk = wave; qbk < nqb; qbk += V2_THREADS / 64) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
-    uint4 qf[C::KCH], dof[C::KCH];
-    load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
-    load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
+    uint4 qf[C::KCH], dof[C::KCH], of[C::KCH];
+    if constexpr (PF) {
+#pragma unroll
+      for (int kc = 0; kc < C::KCH; ++kc) { qf[kc] = qn[kc]; dof[kc] = dn[kc]; of[kc] = on[kc]; }
+      if (qbk + V2_THREADS / 64 < nqb) {
+        const int64_t nq = myq + V2_THREADS / 64 * 16;
+        load_row_regs<T, D>(qn, qb, p.q_st, nq, p.Lq, lane, p.D);
+        load_row_regs<T, D>(dn, dob, p.do_st, nq, p.Lq, lane, p.D);
+        load_row_regs<T, D>(on, obq, p.o_st, nq, p.Lq, lane, p.D);
+      }
+    } else {
+      load_row_regs<T, D>(qf, qb, p.q_st, myq, p.Lq, lane, p.D);
+      load_row_regs<T, D>(dof, dob, p.do_st, myq, p.Lq, lane, p.D);
+      load_row_regs<T, D>(of, obq, p.o_st, myq, p.Lq, lane, p.D);
+    }
     const float lse2 = myq < p.Lq ? p.lse[bh * p.Lq + myq] * LOG2E : INFINITY;
     // delta = rowsum(dO * O) from the dO fragments in registers and the O row (this kernel runs
     // before dK/dV and writes delta for it: no separate delta pass)
     float dlt;
     {
-      uint4 of[C::KCH];
-      load_row_regs<T, D>(of, reinterpret_cast<const T*>(p.o) + b * p.o_sb + h * p.D, p.o_st, myq, p.Lq, lane, p.D);
       float ds = 0.f;
 #pragma unroll
       for (int kc = 0; kc < C::KCH; ++kc) ds += row_chunk_dot<T>(of[kc], dof[kc]);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# x6f grouped tile raster (MMFD_X6F_GROUP_M): fp32 encoder GEMM times interleaved per setting, then FETCH_SIZE
+# x6f grouped tile raster (MMFD_X6F_GROUP_M, an option removed after this measurement: profiles/r04_x6f_raster_ab.log): fp32 encoder GEMM times interleaved per setting, then FETCH_SIZE
 # per dispatch of the forward instantiation for each setting (one --pmc pass each)
 set -e
 cd "$GRAFT_REPO_ROOT"
