@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4: scheduler options on the whole library (AMDGPU register-pressure trackers, relaxed occupancy,
+# no unclustered high-RP reschedule) — GEMM GPU tests per variant, then same-box split-operand (fp32)
+# GEMM A/B against the in-tree build
+set -e
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for v in ftrk frelax fnohrp; do
+  MMFD_LIB_PATH=tools/_ab/$v/libmmfd_hip.so timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "gemm" > gpurun_out/r04r_${v}_test.log 2>&1 || { echo ${v}_TEST_FAILED; tail -20 gpurun_out/r04r_${v}_test.log; exit 1; }
+  echo ${v}_TEST_OK
+  rm -rf gpurun_out/lib_ab
+  AB_WHAT=gemm AB_DTYPE=fp32 AB_LIB=tools/_ab/$v/libmmfd_hip.so bash tools/lib_ab.sh
+  mv gpurun_out/lib_ab gpurun_out/lib_ab_${v}_fp32
+done
