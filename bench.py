@@ -834,7 +834,8 @@ def main():
                                    res["step_peak"][1] + f"; step FLOPs = {GFLOP_PER_PAIR[args.mode]} GFLOP/pair "
                                    "(SURVEY 8(d), algorithmic)"},
             "gemm_ms_per_step": res["gemm_ms"], "gemm_tflops_all_shapes": res["gemm_tf"],
-            "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"],
+            "gemm_kernels": res["gemm_kinds"], "final_loss": res["loss"], "first_step_loss": res["first_loss"],
+            "dp_check": res["dp_check"],
             "peak_memory_gb": res["peak_memory_gb"], "memory": res["memory"],
             "fp32_gemm": ("split operands: x = hi + mid + lo bf16 planes staged together per 32-deep K-step, the six "
                           "bf16 MFMA products per fp32 product accumulated directly into the fp32 accumulator, small "
@@ -853,6 +854,9 @@ def main():
                 out["cpu_baseline"], out["parity"] = cpu_baseline(dev)
             except Exception as e:  # the baseline must never hide the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
+        fx = first_step_parity(args, res)
+        if fx is not None:
+            out.setdefault("parity", {})["first_step_vs_oracle"] = fx
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -871,35 +875,35 @@ def train_leg(args, dev, world, rank, precision):
     tr = build_flagship(dev, precision, freeze_encoders=args.mode == "frozen", dp=dp, seed=42, rank=rank)
     batch = synthetic_batch(args.batch, seed=1000 + rank, device=dev)
 
-    # the whole step as one HIP graph, with N > 1 the RCCL gradient all-reduce included
-    # (MMFD_DP_GRAPH=0: eager DP steps)
-    graphed = not args.no_graph and (world == 1 or os.environ.get("MMFD_DP_GRAPH", "1") == "1")
+    # the whole step as one HIP graph. With N > 1 the eager DP step is the default (MMFD_DP_GRAPH=1
+    # captures the RCCL gradient all-reduce into the graph as well: deterministic since round 5 —
+    # dedicated capture group + thread-local capture mode, mmfd.dp — and self-checked below, but not
+    # yet run on a multi-GPU node)
+    dp_graph = os.environ.get("MMFD_DP_GRAPH", "0") == "1"
+    graphed = not args.no_graph and (world == 1 or dp_graph)
     probe = K.GemmProbe()
     torch.cuda.reset_peak_memory_stats(dev)
     reserved0 = torch.cuda.memory_reserved(dev)
-    if graphed:  # (capture runs its own eager warmup steps first)
-        try:
-            tr.capture(batch, warmup=max(1, args.warmup))
-        except Exception as e:  # a stack that refuses to capture the collectives: eager steps
-            if world == 1:
-                raise
-            log(f"rank {rank}: DP step capture failed ({e!r}); eager steps")
-            tr.release_graph()
-            graphed = False
-    if world > 1 and not args.no_graph and os.environ.get("MMFD_DP_GRAPH", "1") == "1":
-        # every rank runs the same kind of step: if any rank's capture failed, all go eager
-        ok = torch.tensor([1 if graphed else 0], device=dev, dtype=torch.int32)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if graphed and int(ok.item()) == 0:
-            log(f"rank {rank}: another rank's capture failed; eager steps")
-            tr.release_graph()
-            graphed = False
+    first_loss = None
+    dp_check = None
+    if graphed and world > 1:  # capture on every rank, agree, self-check (mmfd.train.capture_dp_step)
+        from mmfd.train import capture_dp_step
+        graphed, dp_check = capture_dp_step(tr, batch, max(1, args.warmup), dev, log=lambda m: log(f"rank {rank}: {m}"))
+        first_loss = getattr(tr, "first_loss", None)
+    elif graphed:  # (capture runs its own eager warmup steps first)
+        tr.capture(batch, warmup=max(1, args.warmup))
+        first_loss = tr.first_loss
     if graphed:
         for _ in range(args.warmup):
             tr.replay()
     else:
-        for _ in range(args.warmup):
-            tr.step(batch)
+        for i in range(args.warmup):
+            loss = tr.step(batch)
+            if first_loss is None:
+                first_loss = loss.clone()
+        if world > 1:  # the same cross-rank checksum on the eager DP step
+            chk = "eager all-reduce verified" if tr.dp.consistent(tr.dp_state()) else "eager all-reduce MISMATCH"
+            dp_check = chk if dp_check is None else f"{dp_check}; {chk}"
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -986,12 +990,38 @@ def train_leg(args, dev, world, rank, precision):
         roof["bf16_mfma_view"] = {"achieved": round(6 * achieved, 1), "peak": PEAK_TFLOPS["bf16"],
                                   "note": "the same launches as executed bf16 MFMA FLOPs (6 x 2MNK) over the bf16 peak"}
     return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
+            "first_loss": None if first_loss is None else [round(v, 6) for v in first_loss.double().cpu().tolist()],
+            "dp_check": dp_check,
             "launch": (("one HIP graph per step (captured fwd + bwd + AdamW" + (" + RCCL gradient all-reduce)" if world > 1
                         else ")") if graphed else "eager kernel launches")
                        + ("; text / image encoders on two streams" if tr_conc else "")
                        + "; GEMM times from 2 eager probe steps after the timed region, encoders serialized"),
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
             "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1), "memory": mem}
+
+
+def first_step_parity(args, res):
+    """The timed workload's first optimizer step against the oracle (tests/golden/config3_bs256_p01.npz,
+    made by tests/golden/make_config3_bs256.py --recipe bench from this bench's own recipe: weights
+    seed 42, batch seed 1000, dropout 0.1 with the kernels' counter-hash masks): the loss vector
+    [total, tt, ti, it, ii] of rank 0's first step, max abs error (bound 1e-3 in
+    tests/test_fullsize_gpu.py). fp32, bs = 256, full fine-tune only; None otherwise."""
+    if args.precision != "fp32" or args.batch != 256 or args.mode != "finetune" or not res.get("first_loss"):
+        return None
+    path = os.path.join(ROOT, "tests", "golden", "config3_bs256_p01.npz")
+    if not os.path.exists(path):
+        return None
+    import numpy as np
+    with np.load(path) as z:
+        want = z["loss"].astype(np.float64)
+        traj = z["loss_steps"][:, 0].tolist() if "loss_steps" in z.files else None
+    got = np.asarray(res["first_loss"], dtype=np.float64)
+    out = {"max_abs_err": float(np.abs(got - want).max()), "got": res["first_loss"],
+           "oracle": [round(float(v), 6) for v in want], "bound": 1e-3,
+           "fixture": "tests/golden/config3_bs256_p01.npz (oracle, chunked whole-batch dropout masks)"}
+    if traj is not None and len(traj) > 1:
+        out["oracle_loss_trajectory"] = [round(float(v), 6) for v in traj]
+    return out
 
 
 def step_peak(precision):

@@ -45,6 +45,10 @@ enum { MMFD_OK = 0, MMFD_ERR_INVALID = 1000, MMFD_ERR_UNSUPPORTED = 1001 };
 /* library                                                                                      */
 /* ------------------------------------------------------------------------------------------- */
 const char* mmfd_last_error_string(void);
+/* ABI version of this header: bumped on every change of an argument struct's layout (2: struct_size
+   at the head of mmfd_gemm_args / mmfd_attn_args, mmfd_attn_args.drop_mask). mmfd_version() returns
+   the library's; a caller compares it with MMFD_ABI_VERSION before its first call. */
+#define MMFD_ABI_VERSION 2
 int mmfd_version(void);
 /* 32-bit dropout hash (host copy of the device function), for tests and the CPU oracle. */
 uint32_t mmfd_dropout_hash(uint64_t seed, uint64_t salt, uint64_t index);
@@ -78,6 +82,9 @@ typedef struct mmfd_epilogue {
 } mmfd_epilogue;
 
 typedef struct mmfd_gemm_args {
+  int64_t struct_size;     /* = sizeof(mmfd_gemm_args) of the caller's header; the library refuses
+                              any other value (MMFD_ERR_INVALID): a caller built against another
+                              layout of this struct fails loudly instead of passing shifted fields */
   int dtype;               /* operand dtype of A and B */
   int trans_a, trans_b;
   int64_t M, N, K;
@@ -105,7 +112,9 @@ typedef struct mmfd_gemm_args {
 
 int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);
 /* bytes of workspace the automatic split choice would like for this problem (incl. the per-split
-   row-sum partials when a_rowsum is set, and the bf16 operand planes of a split-operand fp32 GEMM) */
+   row-sum partials when a_rowsum is set, and the bf16 operand planes of a split-operand fp32 GEMM).
+   This and the two queries below return -1 (mmfd_last_error_string set) for a struct_size other
+   than this header's sizeof(mmfd_gemm_args). */
 int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* args);
 /* the split-K factor mmfd_gemm picks for these arguments (given the workspace it asked for) */
 int mmfd_gemm_splits(const mmfd_gemm_args* args);
@@ -140,6 +149,7 @@ int mmfd_colsum(int dtype, int64_t M, int64_t N, const void* X, int64_t ldx, flo
 /*   O = dropout(P) V ;   lse[b][h][q] = log sum_k exp(S) (fp32)                                */
 /* ------------------------------------------------------------------------------------------- */
 typedef struct mmfd_attn_args {
+  int64_t struct_size;             /* = sizeof(mmfd_attn_args); checked like mmfd_gemm_args.struct_size */
   int dtype;
   int64_t B, H, Lq, Lk, D;         /* D <= 64, D * element size a multiple of 16 B */
   float scale;

@@ -2494,7 +2494,7 @@ void launch_bwd(const AttnP& p, hipStream_t s) {
 }  // namespace
 
 extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
-  MMFD_CHECK_ARG(a != nullptr, "attn_fwd: null args");
+  MMFD_CHECK_STRUCT(a, mmfd_attn_args, "mmfd_attn_fwd");
   AttnP p;
   int rc = fill(*a, p, false);
   if (rc) return rc;
@@ -2532,7 +2532,7 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
 }
 
 extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
-  MMFD_CHECK_ARG(a != nullptr, "attn_bwd: null args");
+  MMFD_CHECK_STRUCT(a, mmfd_attn_args, "mmfd_attn_bwd");
   AttnP p;
   int rc = fill(*a, p, true);
   if (rc) return rc;

@@ -25,6 +25,17 @@ int mmfd_set_error(int code, const char* fmt, ...);
   do {                                                                         \
     if (!(cond)) return mmfd_set_error(MMFD_ERR_INVALID, __VA_ARGS__);        \
   } while (0)
+// ABI guard of the argument structs (include/mmfd.h struct_size): a caller compiled against another
+// layout passes another size and is refused before any field is read
+#define MMFD_CHECK_STRUCT(p, type, what)                                                              \
+  do {                                                                                               \
+    if ((p) == nullptr) return mmfd_set_error(MMFD_ERR_INVALID, "%s: NULL arguments", what);        \
+    if ((p)->struct_size != (int64_t)sizeof(type))                                                   \
+      return mmfd_set_error(MMFD_ERR_INVALID,                                                        \
+                            "%s: " #type ".struct_size = %lld, this library expects %lld (ABI version " \
+                            "%d): rebuild the caller against this include/mmfd.h",                    \
+                            what, (long long)(p)->struct_size, (long long)sizeof(type), MMFD_ABI_VERSION); \
+  } while (0)
 #define MMFD_CHECK_LAUNCH(name)                                                \
   do {                                                                         \
     hipError_t e__ = hipGetLastError();                                        \

@@ -35,6 +35,10 @@ constexpr uint32_t X6_RS = 0x25;   // segments whose A plane appears once (m, l,
 // operand layout of `a` (A / B = the bf16 planes pa / pb, x6.nkt = 32-deep K-steps in all)
 void dispatch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
                   int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6);
+// fp32-output 256x256 GEMMs (gemm_f32out.hip): gemm256_kernel<T, TA, TB, float, false, X6>
+template <typename T, int TA, int TB, bool X6>
+void launch_g8_f32out(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, float* rs_out,
+                      int rs_mode, hipStream_t s, const void* A, int64_t lda, const void* B, int64_t ldb, X6Args x6);
 }  // namespace mmfd_gemmx
 
 namespace {

@@ -15,7 +15,7 @@ int mmfd_set_error(int code, const char* fmt, ...) {
 }
 
 extern "C" const char* mmfd_last_error_string(void) { return g_err; }
-extern "C" int mmfd_version(void) { return 1; }
+extern "C" int mmfd_version(void) { return MMFD_ABI_VERSION; }
 extern "C" uint32_t mmfd_dropout_hash(uint64_t seed, uint64_t salt, uint64_t index) {
   return mmfd_hash(seed, salt, index);
 }

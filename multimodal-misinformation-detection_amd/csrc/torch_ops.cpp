@@ -58,6 +58,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, bool trans_a, bool trans_b, 
           bool a_planes_only = false, bool b_planes_only = false) {
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "mmfd::gemm operands must share a dtype");
   mmfd_gemm_args a{};
+  a.struct_size = sizeof(mmfd_gemm_args);
   a.dtype = dtype_code(A);
   a.trans_a = trans_a;
   a.trans_b = trans_b;
@@ -145,6 +146,7 @@ mmfd_attn_args attn_args(const at::Tensor& q, const at::Tensor& k, const at::Ten
                          int64_t rel_bias_sb, int64_t rel_bias_mod, double dropout_p,
                          const std::optional<at::Tensor>& seed, int64_t salt) {
   mmfd_attn_args a{};
+  a.struct_size = sizeof(mmfd_attn_args);
   a.dtype = dtype_code(q);
   a.B = q.size(0); a.H = heads; a.Lq = q.size(1); a.Lk = k.size(1); a.D = q.size(2) / heads;
   a.scale = (float)scale;

@@ -13,6 +13,19 @@ encoder's backward on its forward's stream, so gradients become ready on two str
 therefore kept per stream: a bucket is packed and handed to RCCL on the stream that produced its
 gradients (RCCL orders a collective after the CURRENT stream only), and the per-step order of the
 collectives is the host order of the backward calls, the same on every rank.
+
+Graph capture of the DP step (FusionTrainer.capture): the captured all-reduces run on a DEDICATED
+process group (`capture_group()`, created with the communicator connected eagerly, so its RCCL
+stream never carries an eager collective), and the capture uses the thread-local error mode. Both
+are needed for the capture not to depend on timing: ProcessGroupNCCL's watchdog thread polls the
+events of every eager collective of a group; in the global capture mode any such query from the
+watchdog during a capture is refused (hipErrorStreamCaptureUnsupported), and an event last recorded
+on a stream that has since joined a capture is refused as well (hipErrorCapturedEvent) — the two
+aborts of round 4. With the eager collectives on the default group's stream and the captured ones
+on the capture group's stream, and the watchdog's queries allowed by the thread-local mode, no
+query can hit a capturing stream whenever it happens. `consistent()` is the self-check afterwards:
+after one replay every rank must hold bitwise-identical gradients and parameters (ranks train on
+different batches, so that holds only if the captured all-reduce really ran).
 """
 from __future__ import annotations
 
@@ -20,6 +33,34 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
+
+
+def state_checksum(tensors) -> torch.Tensor:
+    """int64 checksum of the exact bits of `tensors` (None entries skipped), on their device: the
+    integer sum of each tensor's words (wrapping, so the order of the additions does not matter)
+    times an odd per-position weight — equal tensors in the same order give equal checksums, and a
+    tensor that differs in any bit almost never does."""
+    acc = None
+    for i, t in enumerate(tensors):
+        if t is None:
+            continue
+        t = t.detach().contiguous().reshape(-1)
+        words = t.view(torch.int32) if t.element_size() == 4 else t.view(torch.int16) if t.element_size() == 2 \
+            else t.view(torch.int64) if t.element_size() == 8 else t.view(torch.uint8)
+        s = words.to(torch.int64).sum() * (2 * i + 1)
+        acc = s if acc is None else acc + s
+    if acc is None:
+        acc = torch.zeros((), dtype=torch.int64)
+    return acc.reshape(1)
+
+
+def ranks_agree(value: torch.Tensor, group=None) -> bool:
+    """True when `value` (an int64 tensor) is identical on every rank of `group`: its MIN and its
+    MAX over the ranks are equal. Every rank gets the same answer."""
+    lo, hi = value.clone(), value.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    return bool(torch.equal(lo, hi))
 
 
 def _pack(g, dst):
@@ -41,6 +82,7 @@ class GradAllReduce:
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
         self.group = group
         self.force = bool(force)
+        self._capture_group = None
         self._bufs = {}
         self._pack, self._unpack = pack, unpack
         self.last_buckets = {}
@@ -129,7 +171,36 @@ class GradAllReduce:
         self.ready((p, p.grad) for p in params)
         self.finish()
 
+    # ---- graph capture -------------------------------------------------------------------------------
+    def capture_group(self):
+        """The process group the captured step's all-reduces run on (collective: every rank calls it
+        at the same point; created once). Same ranks as `group`; with a device-bound default group
+        (init_process_group(device_id=...), as bench.py and train.py do) its communicator is
+        connected at creation, so no collective ever runs on it outside a capture."""
+        if self._capture_group is None:
+            ranks = None if self.group is None else dist.get_process_group_ranks(self.group)
+            self._capture_group = dist.new_group(ranks=ranks, group_desc="mmfd_dp_capture")
+        return self._capture_group
+
+    def use_capture_group(self, on: bool = True):
+        """route this object's collectives to capture_group() (on) or back to `group` (off)"""
+        self._use_capture = bool(on)
+        if on:
+            self.capture_group()
+
+    def consistent(self, tensors) -> bool:
+        """Cross-rank self-check: True when every rank holds bitwise-identical `tensors` (gradients
+        and parameters after a data-parallel step); every rank gets the same answer. Runs eager
+        collectives on `group`."""
+        if not dist.is_initialized():
+            return True
+        c = state_checksum(tensors)
+        return ranks_agree(c, self.group)
+
     # ---- internals -----------------------------------------------------------------------------------
+    def _coll_group(self):
+        return self._capture_group if getattr(self, "_use_capture", False) else self.group
+
     def _active(self):
         return dist.is_initialized() and (self.force or dist.get_world_size(self.group) > 1)
 
@@ -147,5 +218,5 @@ class GradAllReduce:
         for _, g in items:
             self._pack(g, buf[off:off + g.numel()])
             off += g.numel()
-        work = dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        work = dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=self._coll_group(), async_op=True)
         self._works.append((work, items, buf))

@@ -26,6 +26,7 @@ LIB_PATH = os.environ.get("MMFD_LIB_PATH") or os.path.join(_HERE, "libmmfd_hip.s
 TORCH_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libmmfd_torch.so")
 
 F32, BF16, F16 = 0, 1, 2
+ABI_VERSION = 2  # include/mmfd.h MMFD_ABI_VERSION: the layout of the argument structs below
 COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
 
@@ -48,8 +49,19 @@ class EpilogueArgs(ctypes.Structure):
     ]
 
 
-class GemmArgs(ctypes.Structure):
+class _Sized(ctypes.Structure):
+    """argument structs that start with `struct_size` (include/mmfd.h, ABI version 2): set on
+    construction, so the library can refuse a caller built against another layout"""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        if "struct_size" not in kw:
+            self.struct_size = ctypes.sizeof(self)
+
+
+class GemmArgs(_Sized):
     _fields_ = [
+        ("struct_size", ctypes.c_int64),
         ("dtype", ctypes.c_int), ("trans_a", ctypes.c_int), ("trans_b", ctypes.c_int),
         ("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
         ("A", ctypes.c_void_p), ("lda", ctypes.c_int64),
@@ -65,8 +77,9 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
-class AttnArgs(ctypes.Structure):
+class AttnArgs(_Sized):
     _fields_ = [
+        ("struct_size", ctypes.c_int64),
         ("dtype", ctypes.c_int),
         ("B", ctypes.c_int64), ("H", ctypes.c_int64), ("Lq", ctypes.c_int64), ("Lk", ctypes.c_int64),
         ("D", ctypes.c_int64),
@@ -187,6 +200,9 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mmfd_version() != ABI_VERSION:
+        raise NativeLibraryError(f"{path} implements ABI version {lib.mmfd_version()}, these bindings version "
+                                 f"{ABI_VERSION}: rebuild (python -c 'import __graft_entry__ as g; g.build()')")
     if not os.path.exists(TORCH_LIB_PATH):
         raise NativeLibraryError(f"{TORCH_LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'`")
     try:

@@ -14,7 +14,6 @@ from __future__ import annotations
 import argparse
 import logging
 import os
-import time
 
 import numpy as np
 import torch
@@ -223,29 +222,55 @@ class FusionTrainer:
         replays. With data parallelism (`dp`) the gradient all-reduce is captured too: the per-
         stream bucket packs, the RCCL all_reduce kernels (ProcessGroupNCCL keeps captured work out of
         its watchdog) and finish()'s wait + unpack become nodes of the same graph; the buckets were
-        allocated by the eager warm-up steps, so the graph reads and writes fixed addresses."""
+        allocated by the eager warm-up steps, so the graph reads and writes fixed addresses.
+
+        No timing assumption (round 4 slept 0.5 s here): the captured all-reduces go to the DP
+        object's dedicated capture group, whose RCCL stream never carried an eager collective, and
+        the capture runs in the thread-local error mode, under which the watchdog thread's event
+        queries of the eager collectives (default group, never captured) stay legal (mmfd.dp).
+        `first_loss` keeps the loss vector of the first warm-up step (the first optimizer step of
+        this trainer when it is fresh)."""
         self._static = batch
         s = torch.cuda.Stream(device=self._device())
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(warmup):  # optimizer state, weight shadows, kernel attributes
-                self.step(batch)
+            for i in range(warmup):  # optimizer state, weight shadows, kernel attributes
+                loss = self.step(batch)
+                if i == 0:
+                    self.first_loss = loss.clone()
         torch.cuda.current_stream().wait_stream(s)
-        if self.dp is not None and self.dp._active():
-            # ProcessGroupNCCL's watchdog thread polls the eager warm-up's collectives (their events
-            # on RCCL's stream) every ~100 ms; RCCL's stream joins the capture with the first
-            # captured all-reduce, and a poll that lands inside the capture aborts the process
-            # (hipErrorCapturedEvent / hipErrorStreamCaptureUnsupported, 2 of 4 world-1 runs): let
-            # the watchdog retire every eager collective before capturing
+        dp_on = self.dp is not None and self.dp._active()
+        if dp_on:
             torch.cuda.synchronize()
-            time.sleep(float(os.environ.get("MMFD_DP_QUIESCE_S", "0.5")))
+            self.dp.use_capture_group(True)
         self.optimizer.prepare_capture()  # pointer tables outside the graph's memory pool
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._graph_loss = self.step(batch)
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._graph_loss = self.step(batch)
+        finally:
+            if dp_on:
+                self.dp.use_capture_group(False)
         self.optimizer.finalize_capture()
         self._graph = g
         return self
+
+    def verify_capture(self, batch=None):
+        """Self-check of the captured data-parallel step: one replay, then every rank compares a
+        checksum of all its gradients and parameters with the others (mmfd.dp.GradAllReduce.
+        consistent: MIN == MAX over the ranks). The ranks train on different batches, so the
+        averaged gradients — and the parameters AdamW moves with them — are bitwise equal on every
+        rank only if the captured all-reduce really ran. True without data parallelism."""
+        if self.dp is None or not self.dp._active():
+            return True
+        self.replay(batch)
+        torch.cuda.synchronize()
+        return self.dp.consistent(self.dp_state())
+
+    def dp_state(self):
+        """the tensors every rank must agree on after a data-parallel step: the trained parameters'
+        gradients, then all parameters"""
+        return [p.grad for p in self.params] + [p for p in self.params]
 
     def release_graph(self):
         """drop the captured step and its private memory pool (eager steps afterwards)"""
@@ -280,12 +305,55 @@ class FusionTrainer:
                 m.train(w)
 
 
+def capture_dp_step(tr, batch, warmup, device, log=logger.info):
+    """Capture the data-parallel step on every rank and agree on it (bench.py with MMFD_DP_GRAPH=1).
+    Returns (graphed, check): every rank gets the same answer. A rank whose capture raises goes
+    eager, and then all do (MIN over the ranks of a success flag); a captured step whose replay
+    leaves the ranks with different gradients or parameters (FusionTrainer.verify_capture: the
+    captured all-reduce did not run, or not in step) is released on every rank as well."""
+    import torch.distributed as dist
+    ok = True
+    try:
+        tr.capture(batch, warmup=warmup)
+    except Exception as e:  # a stack that refuses to capture the collectives
+        log(f"DP step capture failed ({e!r}); eager steps")
+        ok = False
+    flag = torch.tensor([1 if ok else 0], device=device, dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        tr.release_graph()
+        return False, "capture failed on a rank: eager steps"
+    if not tr.verify_capture():
+        log("captured DP step failed the cross-rank checksum; eager steps on every rank")
+        tr.release_graph()
+        return False, "captured all-reduce MISMATCH: eager steps"
+    return True, "captured all-reduce verified"
+
+
 def _detach_outs(o):
     if torch.is_tensor(o):
         return o.detach()
     if isinstance(o, (tuple, list)):
         return type(o)(_detach_outs(x) for x in o)
     return o
+
+
+def flagship_modules(seed=42, dropout=0.1, encoder_dropout=None):
+    """(text, image, head) of the flagship on the CPU, initialised from `seed` exactly as
+    build_flagship does (the weights tests/golden/make_config3_bs256.py gives the oracle)"""
+    torch.manual_seed(seed)
+    bc = BertConfig() if encoder_dropout is None else BertConfig(hidden_dropout_prob=encoder_dropout,
+                                                                  attention_probs_dropout_prob=encoder_dropout)
+    text = BertModel(bc)
+    image = ViTModel(ViTConfig())
+    head = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768, embed_dim=256, num_heads=8,
+                                        dropout=dropout, hidden_dim=64, num_classes=3)
+    return text, image, head
+
+
+def flagship_dropout_seeds(seed=42, rank=0):
+    """(text encoder, head) dropout seeds of build_flagship's rank `rank` (advanced by one per step)"""
+    return seed + 7919 * rank, seed + 1 + 7919 * rank
 
 
 def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders=False, lr=1e-4, dp=None,
@@ -296,15 +364,10 @@ def build_flagship(device="cuda", precision="bf16", dropout=0.1, freeze_encoders
     (model.py dropout=0.1); the encoders keep their HF configs' own (BERT 0.1, ViT 0.0).
     `encoder_dropout` overrides BERT's only: ViT-B/16 trains without dropout, and mmfd's ViT
     implements only that configuration (a ViTConfig with dropout raises in training)."""
-    torch.manual_seed(seed)
-    bc = BertConfig() if encoder_dropout is None else BertConfig(hidden_dropout_prob=encoder_dropout,
-                                                                  attention_probs_dropout_prob=encoder_dropout)
-    text = BertModel(bc).to(device)
-    image = ViTModel(ViTConfig()).to(device)
-    head = MisinformationDetectionModel(text_input_dim=768, image_input_dim=768, embed_dim=256, num_heads=8,
-                                        dropout=dropout, hidden_dim=64, num_classes=3).to(device)
-    text.manual_seed(seed + 7919 * rank)
-    head.manual_seed(seed + 1 + 7919 * rank)
+    text, image, head = (m.to(device) for m in flagship_modules(seed, dropout, encoder_dropout))
+    st, sh = flagship_dropout_seeds(seed, rank)
+    text.manual_seed(st)
+    head.manual_seed(sh)
     return FusionTrainer(text, image, head, lr=lr, freeze_encoders=freeze_encoders, precision=precision, dp=dp)
 
 

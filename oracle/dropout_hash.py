@@ -62,12 +62,42 @@ def salt_of(name: str) -> int:
     return (zlib.crc32(b) << 32) | zlib.crc32(b[::-1] + b"mmfd")
 
 
+def keep_mask_rows(seed: int, salt: int, shape, p: float, rows):
+    """Keep-mask of a batch-major contiguous tensor of `shape` that holds the batch rows `rows` of a
+    larger whole batch: element e of batch row r has the whole-batch flat index
+    rows[r] * inner + e (inner = numel / len(rows)) — the index the HIP kernels hash when they run
+    the whole batch at once. rows = arange(R) is keep_mask."""
+    rows = np.asarray(rows, dtype=np.uint64)
+    n = int(np.prod(shape))
+    assert n % len(rows) == 0, (shape, len(rows))
+    inner = n // len(rows)
+    idx = rows[:, None] * np.uint64(inner) + np.arange(inner, dtype=np.uint64)[None, :]
+    h = dropout_hash(seed, salt, idx.reshape(-1))
+    return (h >= np.uint32(drop_threshold(p))).reshape(shape)
+
+
+class Drop:
+    """`drop(site, x)` callback for the oracle: applies exactly the HIP kernels' mask. With `rows`
+    (the whole-batch row indices of this call's batch rows, see keep_mask_rows) a chunk of a larger
+    batch gets the masks the whole batch gets at those rows: oracle.train_step.chunked_loss_grads
+    binds one per chunk for the encoders (stacked claim|evidence rows [s:e] and [B+s:B+e]) and one
+    for the head (rows [s:e])."""
+
+    def __init__(self, seed: int, p: float, rows=None):
+        self.seed, self.p, self.rows = int(seed), float(p), rows
+
+    def with_rows(self, rows):
+        return Drop(self.seed, self.p, rows)
+
+    def __call__(self, site, x):
+        import torch
+        if self.rows is None:
+            keep = keep_mask(self.seed, salt_of(site), tuple(x.shape), self.p)
+        else:
+            keep = keep_mask_rows(self.seed, salt_of(site), tuple(x.shape), self.p, self.rows)
+        return x * torch.from_numpy(keep).to(x.dtype) / (1.0 - self.p)
+
+
 def make_drop(seed: int, p: float, dtype=None):
     """`drop(site, x)` callback for the oracle: applies exactly the HIP kernels' mask."""
-    import torch
-
-    def drop(site, x):
-        keep = torch.from_numpy(keep_mask(seed, salt_of(site), tuple(x.shape), p))
-        return x * keep.to(x.dtype) / (1.0 - p)
-
-    return drop
+    return Drop(seed, p)

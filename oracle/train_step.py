@@ -82,15 +82,23 @@ class OracleTrainer:
 
 
 def chunked_loss_grads(bert_p, vit_p, head_p, batch, *, bert_cfg=BERT_BASE, vit_cfg=VIT_B16, num_heads=8, chunk=8,
-                       drop=None, progress=None):
+                       drop=None, drop_head=None, progress=None):
     """The loss and parameter gradients of ONE step on a large batch (train.py:146-170 with
     trainable encoders: Σ over the 4 paths of the batch-mean cross-entropy), computed in chunks of
     `chunk` pairs so the CPU autograd graph stays small: chunk c contributes n_c / B of its own
-    mean loss, so the accumulated gradients are those of the whole-batch mean. Returns
-    (total, [4 path losses], {"bert."/"vit."/"head." + name: grad})."""
+    mean loss, so the accumulated gradients are those of the whole-batch mean.
+
+    Dropout (layers.py:15,17,53; the encoders' hidden / attention dropout): `drop` for the text
+    encoder and `drop_head` for the fusion head (default: `drop`), oracle.dropout_hash.Drop
+    callbacks. Each chunk binds them to its whole-batch rows — the encoder's stacked rows [s:e] and
+    [B+s:B+e], the head's rows [s:e] — so every chunk hashes the flat indices the HIP kernels hash
+    for the whole batch at once, and the chunked masks are exactly the whole-batch masks.
+    Returns (total, [4 path losses], {"bert."/"vit."/"head." + name: grad})."""
+    import numpy as np
     bp = {k: v.clone().float().requires_grad_(True) for k, v in bert_p.items()}
     vp = {k: v.clone().float().requires_grad_(True) for k, v in vit_p.items()}
     hp = {k: v.clone().float().requires_grad_(True) for k, v in head_p.items()}
+    drop_head = drop if drop_head is None else drop_head
     B = batch["labels"].shape[0]
     total = torch.zeros((), dtype=torch.float64)
     per = torch.zeros(4, dtype=torch.float64)
@@ -100,11 +108,13 @@ def chunked_loss_grads(bert_p, vit_p, head_p, batch, *, bert_cfg=BERT_BASE, vit_
         ids = torch.cat([batch["input_ids"][s:e], batch["input_ids"][B + s:B + e]])
         mask = torch.cat([batch["attention_mask"][s:e], batch["attention_mask"][B + s:B + e]])
         px = torch.cat([batch["pixel_values"][s:e], batch["pixel_values"][B + s:B + e]])
+        de = None if drop is None else drop.with_rows(np.concatenate([np.arange(s, e), np.arange(B + s, B + e)]))
+        dh = None if drop_head is None else drop_head.with_rows(np.arange(s, e))
         T = OE.bert_forward(bp, ids, mask, None, num_layers=bert_cfg["num_hidden_layers"],
-                            num_heads=bert_cfg["num_attention_heads"], drop=drop)
+                            num_heads=bert_cfg["num_attention_heads"], drop=de)
         I = OE.vit_forward(vp, px, num_layers=vit_cfg["num_hidden_layers"],
                            num_heads=vit_cfg["num_attention_heads"], patch=vit_cfg["patch_size"])
-        out = OF.model_forward(hp, T[:n], I[:n], T[n:], I[n:], num_heads=num_heads, drop=drop)
+        out = OF.model_forward(hp, T[:n], I[:n], T[n:], I[n:], num_heads=num_heads, drop=dh)
         t, pl = OF.path_loss(out, batch["labels"][s:e])
         (t * (n / B)).backward()
         total += t.detach().double() * (n / B)

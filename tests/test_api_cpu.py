@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in K.SIGNATURES, f"{s} declared in include/mmfd.h but not bound in kernels.py"
-    assert lib.mmfd_version() >= 1
+    assert lib.mmfd_version() == K.ABI_VERSION == 2
 
 
 def test_host_hash_matches_oracle():
@@ -44,6 +44,31 @@ def test_error_reporting_without_gpu_compute():
     a.dtype = 7
     rc = K.lib().mmfd_gemm(a, None)
     assert rc != 0 and b"dtype" in K.lib().mmfd_last_error_string()
+
+
+def test_struct_of_another_abi_layout_is_refused():
+    """a caller built against another layout of mmfd_gemm_args / mmfd_attn_args
+    (e.g. round 3's attention struct, 8 bytes shorter before drop_mask) passes another struct_size
+    and is refused before any field is read, with a clear error string."""
+    import ctypes
+    lib = K.lib()
+    a = K.GemmArgs()
+    assert a.struct_size == ctypes.sizeof(K.GemmArgs)
+    a.struct_size -= 8  # a shorter struct
+    a.dtype = K.BF16
+    assert lib.mmfd_gemm(a, None) == 1000  # MMFD_ERR_INVALID
+    msg = lib.mmfd_last_error_string().decode()
+    assert "struct_size" in msg and "ABI version 2" in msg, msg
+    assert lib.mmfd_gemm_workspace_bytes(a) == -1 and lib.mmfd_gemm_splits(a) == -1 and lib.mmfd_gemm_runs_split(a) == -1
+    for fn in (lib.mmfd_attn_fwd, lib.mmfd_attn_bwd):
+        t = K.AttnArgs()
+        t.struct_size = ctypes.sizeof(K.AttnArgs) - 8
+        assert fn(t, None) == 1000
+        assert "mmfd_attn_args.struct_size" in lib.mmfd_last_error_string().decode()
+    # the right size passes the guard (and then fails on its own argument checks, as before)
+    b = K.GemmArgs()
+    b.dtype = 7
+    assert lib.mmfd_gemm(b, None) != 0 and b"bad dtype" in lib.mmfd_last_error_string()
 
 
 @pytest.mark.parametrize("kw,fixture_key", [({}, "param_names"), ({"factify": True, "num_classes": 5}, "factify_param_names"),

@@ -136,3 +136,74 @@ def test_replicas_from_different_seeds_stay_identical():
     for a, b in zip(res[0][1], res[1][1]):
         assert (a == b).all()
     assert any((a != b).any() for a, b in zip(res[0][0], res[0][1]))  # and training moved them
+
+
+def _check_worker(rank, world, port, q):
+    """mmfd.dp.state_checksum / GradAllReduce.consistent and mmfd.train.capture_dp_step over gloo:
+    identical tensors agree, a one-bit difference on one rank does not, and a captured step whose
+    replay leaves the ranks different (or whose capture failed on one rank) is released on EVERY rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mmfd.dp import GradAllReduce, state_checksum
+        from mmfd.train import capture_dp_step
+
+        dp = GradAllReduce(pack=_pack, unpack=_unpack)
+        g = torch.Generator().manual_seed(3)
+        same = [torch.randn(17, 5, generator=g), None, torch.randn(300, generator=g).bfloat16(),
+                torch.arange(7, dtype=torch.int64)]
+        res = {"same": dp.consistent(same)}
+        flipped = [t.clone() if t is not None else None for t in same]
+        if rank == 1:  # one bit of one element on one rank
+            flipped[0].view(torch.int32)[3, 2] ^= 1
+        res["flipped"] = dp.consistent(flipped)
+        swapped = [same[2], None, same[0], same[3]] if rank == 1 else same  # same tensors, other order
+        res["swapped"] = dp.consistent(swapped)
+        res["sum_order_free"] = bool(torch.equal(state_checksum([same[0]]), state_checksum([same[0].flip(0).flip(0)])))
+
+        class FakeTrainer:
+            """capture / verify / release as FusionTrainer; `mismatch` makes rank 1's replay differ"""
+            def __init__(self, fail_capture=False, mismatch=False):
+                self.fail_capture, self.mismatch, self.released, self.dp = fail_capture, mismatch, False, dp
+                self.p = torch.ones(4)
+
+            def capture(self, batch, warmup):
+                if self.fail_capture and rank == 0:
+                    raise RuntimeError("capture refused")
+
+            def verify_capture(self):
+                if self.mismatch and rank == 1:
+                    self.p[0] += 1.0  # the all-reduce "did not run": rank 1's state differs
+                return self.dp.consistent([self.p])
+
+            def release_graph(self):
+                self.released = True
+
+        for name, kw in (("ok", {}), ("mismatch", {"mismatch": True}), ("capture_fail", {"fail_capture": True})):
+            t = FakeTrainer(**kw)
+            graphed, msg = capture_dp_step(t, None, 1, "cpu", log=lambda m: None)
+            res["dp_" + name] = (graphed, t.released, msg)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cross_rank_checksum_and_capture_fallback_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        got = res[r]
+        assert got["same"] is True and got["flipped"] is False and got["swapped"] is False
+        assert got["sum_order_free"]
+        assert got["dp_ok"][:2] == (True, False), got["dp_ok"]
+        # the mismatch branch: both ranks release the graph and run eager steps, whichever differed
+        assert got["dp_mismatch"][:2] == (False, True) and "MISMATCH" in got["dp_mismatch"][2], got["dp_mismatch"]
+        assert got["dp_capture_fail"][:2] == (False, True), got["dp_capture_fail"]

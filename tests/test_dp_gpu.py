@@ -285,7 +285,10 @@ def _worker_nccl_graph(port, q):
                                                           float((x - y).abs().max()) > tol * max(1.0, float(y.abs().max()))):
                             bad.append(n)
                 ok.append((float((la - lb).abs().max()), bad[:8]))
-            out[name] = (ok, dict(a.dp.last_buckets))
+            buckets = dict(a.dp.last_buckets)
+            # the bench's self-check of a captured DP step (one more replay, then the cross-rank
+            # checksum of gradients + parameters; trivially equal with one rank, run for the code path)
+            out[name] = (ok, buckets, a.verify_capture())
             a.release_graph()
             b.release_graph()
         q.put(out)
@@ -303,7 +306,9 @@ def test_dp_nccl_world1_graph_captured_step():
     ProcessGroupNCCL (RCCL) with one rank. Replayed on new batches it must equal the plain captured
     step (no DP) in losses, gradients and updated parameters, bit for bit (the word-embedding
     gradient, accumulated with fp32 atomics, within 1e-6), tiny with 50 KB buckets and full size
-    with the default 32 MB buckets, dropout on."""
+    with the default 32 MB buckets, dropout on. Since round 5 the captured all-reduces run on the DP
+    object's dedicated capture group in the thread-local capture mode (no quiesce sleep before the
+    capture; mmfd.dp), and the bench's cross-rank self-check (verify_capture) runs on it."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl_graph, args=(_free_port(), q))
@@ -311,7 +316,8 @@ def test_dp_nccl_world1_graph_captured_step():
     out = _collect([p], q, 1)[0]
     assert "error" not in out, out.get("error")
     assert p.exitcode == 0
-    for name, (steps, nb) in out.items():
+    for name, (steps, nb, verified) in out.items():
         for lerr, bad in steps:
             assert lerr == 0.0 and not bad, (name, lerr, bad)
         assert len(nb) == 2 and sum(nb.values()) >= 2, (name, nb)
+        assert verified, name

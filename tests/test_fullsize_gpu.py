@@ -131,9 +131,7 @@ def test_config3_bs256_step_matches_oracle():
     max |g|, ||g|| and 512 strided gradient samples).
       loss vector <= 1e-3 abs (north_star); per tensor: samples <= 2e-3 of max(|g| max, 1e-3 of the
       largest gradient), max |g| and ||g|| within 2e-3 relative."""
-    import numpy as np
-
-    from tests.golden.make_config3_bs256 import B, BATCH_SEED, WEIGHT_SEED, sample_index
+    from tests.golden.make_config3_bs256 import B, BATCH_SEED, WEIGHT_SEED
     fx = _fixture("config3_bs256.npz")
     torch.cuda.empty_cache()
     tr, states = build_pair("fp32", dropout=0.0, cfg=FULL, seed=WEIGHT_SEED, lr=1e-4, with_oracle=False)
@@ -159,9 +157,21 @@ def test_config3_bs256_step_matches_oracle():
     step_gib = (torch.cuda.max_memory_allocated(dev) - base) / 2**30
     print(f"config3 bs=256 eager step: {step_gib:.1f} GiB above the {base / 2**30:.1f} GiB before it")
     assert step_gib <= 175.0, step_gib
+    _compare_bs256(tr, fx, loss, names, "config3 bs=256 fp32")
+    del tr
+    torch.cuda.empty_cache()
+
+
+def _compare_bs256(tr, fx, loss, names, what):
+    """loss vector <= 1e-3 abs; per tensor: 512 strided gradient samples <= 2e-3 of max(|g| max,
+    1e-3 of the largest gradient), max |g| and ||g|| within 2e-3 relative"""
+    import numpy as np
+
+    from tests.golden.make_config3_bs256 import sample_index
+    from tests.smoke_impl import _named
+    dev = torch.device("cuda", 0)
     lerr = np.abs(loss.double().cpu().numpy() - fx["loss"]).max()
     assert lerr <= 1e-3, (loss.tolist(), fx["loss"].tolist())
-    from tests.smoke_impl import _named
     mine = _named(tr)
     assert set(names) <= set(mine), set(names) - set(mine)
     floor = 1e-3 * float(fx["gmax"].max())
@@ -182,9 +192,37 @@ def test_config3_bs256_step_matches_oracle():
             fails.append(f"{n}: samples {e:.2e} max {em:.2e} norm {en:.2e}")
         if e > worst:
             worst, wname = e, n
-    print(f"config3 bs=256 fp32: loss err {lerr:.3e}, worst sampled grad err {worst:.3e} ({wname}), "
-          f"{len(names)} tensors")
+    print(f"{what}: loss err {lerr:.3e}, worst sampled grad err {worst:.3e} ({wname}), {len(names)} tensors")
     assert not fails, "; ".join(fails[:8])
+
+
+def test_config3_bs256_dropout_step_matches_oracle():
+    """the bench's OWN timed workload pinned against the oracle — the flagship's
+    weights (build_flagship(seed=42)), bench.py's synthetic batch (bs = 256, seed 1000), fp32, training
+    mode with dropout 0.1 in BERT (hidden + attention probabilities) and in the fusion head, one full
+    fine-tune step. The oracle (tests/golden/make_config3_bs256.py --recipe bench) computes the batch
+    in 8-pair chunks with each chunk's masks bound to its whole-batch rows (oracle.dropout_hash.Drop),
+    i.e. exactly the counter-hash masks the kernels draw for the whole batch at once
+    (tests/test_oracle_chunked_cpu.py). Bounds as the dropout-0 test: loss <= 1e-3, sampled
+    gradients <= 2e-3 of the tensor max."""
+    from mmfd.dataset import synthetic_batch
+    from mmfd.train import build_flagship
+    from tests.golden.make_config3_bs256 import B, BENCH_BATCH_SEED, BENCH_P, BENCH_SEED
+    fx = _fixture("config3_bs256_p01.npz")
+    assert str(fx["recipe"]) == "bench"
+    torch.cuda.empty_cache()
+    dev = torch.device("cuda", 0)
+    tr = build_flagship(dev, "fp32", dropout=BENCH_P, seed=BENCH_SEED, rank=0)
+    from tests.smoke_impl import _named
+    mine = _named(tr)
+    names = [str(n) for n in fx["names"]]
+    for i, n in enumerate(names):  # the fixture was made from these exact initial weights
+        w = mine[n].detach().double()
+        assert abs(w.sum().item() - fx["init_sum"][i]) <= 1e-9 * max(1.0, fx["init_abs"][i]), f"stale fixture: {n}"
+    batch = synthetic_batch(B, seed=BENCH_BATCH_SEED, device=dev)
+    loss = tr.step(batch)
+    torch.cuda.synchronize()
+    _compare_bs256(tr, fx, loss, names, "config3 bs=256 fp32 dropout 0.1 (bench workload)")
     del tr
     torch.cuda.empty_cache()
 
