@@ -20,8 +20,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+# torch is imported in main(), not here: the corpus build's decode workers (mmfd.hostdecode, forkserver
+# children) re-import this script as __mp_main__ and must stay torch-free
+torch = dist = None
 
 METRIC = "claim–evidence pairs/sec (fwd+bwd) at bs=256; 1/2/4/8 MI355X scaling"
 GFLOP_PER_PAIR = {"finetune": 351.18, "frozen": 121.11}  # BASELINE.md §3 (FlopCounterMode, fwd+bwd)
@@ -760,6 +761,9 @@ def preembed_image_main(args, dev, world, rank):
 
 
 def main():
+    global torch, dist
+    import torch
+    import torch.distributed as dist
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)

@@ -395,12 +395,20 @@ class ImageCorpus:
         if not chunks:
             return out
         ex = self.feature_extractor
+        ring = None
         if (self.decode == "processes" and self.decode_workers > 1 and hasattr(ex, "preprocess_device")
                 and torch.device(ex.device).type == "cuda"):
+            from .hostdecode import RingUnavailable
+            try:
+                ring = self._decode_ring()
+            except RingUnavailable as err:  # no shared memory / page locking here: the process pool
+                import warnings
+                warnings.warn(f"{err}; decoding through the process pool instead")
+                self.decode_ring_error = str(err)
+        if ring is not None:
             # the workers decode into a page-locked shared ring, the batch's pixels go to the device
             # with asynchronous copies, and the features stay on the device until the build is done:
             # the host thread only submits and enqueues, so decode, upload and the GPU overlap
-            ring = self._decode_ring()
             h = ring.submit(chunks[0], 0)
             feats = []
             for ci, chunk in enumerate(chunks):

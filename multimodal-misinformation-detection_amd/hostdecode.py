@@ -79,6 +79,10 @@ class DecodePool:
 
 
 # ---- decode straight into page-locked shared memory (no host copies in the caller) -------------------
+class RingUnavailable(RuntimeError):
+    """the page-locked shared-memory ring cannot be set up on this host"""
+
+
 def _release_ring(ex, shm, addr, device):
     ex.shutdown(wait=True, cancel_futures=True)
     try:
@@ -104,27 +108,37 @@ class PinnedDecodeRing:
     stream has consumed its copies (an event per slot). Images that do not fit their group's space
     come back through the pipe and are uploaded from ordinary memory."""
 
-    def __init__(self, batch, device, workers=None, group=8, cap=1 << 20, slots=2):
+    def __init__(self, batch, device, workers=None, group=8, cap=None, slots=2):
+        """`cap`: ring bytes per image (default env MMFD_DECODE_RING_CAP or 1 MiB — a 512x512 RGB
+        image is 0.75 MiB; larger images come back through the pipe). The ring is slots x batch x cap
+        bytes of /dev/shm, page-locked: raises RingUnavailable when the shared memory or the page
+        locking cannot be had (the caller then decodes with the process pool or threads)."""
         import concurrent.futures as cf
         import ctypes
         import multiprocessing as mp
 
         import torch
+        if cap is None:
+            cap = int(os.environ.get("MMFD_DECODE_RING_CAP", 1 << 20))
         self.device = torch.device(device)
         self.workers = int(workers or min(16, len(os.sched_getaffinity(0))))
         self.group, self.slots = max(1, int(group)), int(slots)
         self.gbytes = self.group * int(cap)
         self.gps = (int(batch) + self.group - 1) // self.group
         self.sbytes = self.gps * self.gbytes
-        self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self.sbytes)
+        try:
+            self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self.sbytes)
+        except OSError as e:  # e.g. a small /dev/shm in a container
+            raise RingUnavailable(f"decode ring: {self.slots * self.sbytes} B of shared memory: {e}") from e
         self._addr = ctypes.addressof(ctypes.c_char.from_buffer(self.shm.buf))
         rc = torch._C._cudart.cudaHostRegister(self._addr, self.slots * self.sbytes, 0)
         if int(rc) != 0:
             self.shm.close()
             self.shm.unlink()
-            raise RuntimeError(f"hipHostRegister of the decode ring failed ({rc})")
+            raise RingUnavailable(f"hipHostRegister of the decode ring failed ({rc})")
         self.host = torch.frombuffer(self.shm.buf, dtype=torch.uint8)
         self._events = [None] * self.slots
+        self._writers = [None] * self.slots  # the decode futures that write into each slot
         ctx = mp.get_context("forkserver")
         ctx.set_forkserver_preload(["mmfd_decode_worker", "PIL.Image"])
         self._ex = cf.ProcessPoolExecutor(max_workers=self.workers, mp_context=ctx)
@@ -134,6 +148,14 @@ class PinnedDecodeRing:
                                      exitpriority=10)
 
     def submit(self, paths, slot):
+        import concurrent.futures as cf
+        prev = self._writers[slot]
+        if prev is not None:
+            # every decode task that writes this slot has finished — also when its batch was never
+            # uploaded (a build that stopped between submit and upload): no stale write can land
+            # after the new batch's
+            cf.wait(prev)
+            self._writers[slot] = None
         ev = self._events[slot]
         if ev is not None:
             ev.synchronize()  # the previous batch's copies out of this slot have run
@@ -141,9 +163,11 @@ class PinnedDecodeRing:
         paths = list(paths)
         if len(paths) > self.gps * self.group:
             raise ValueError("batch larger than the ring slot")
-        return [self._ex.submit(_dw.decode_group_into, self.shm.name, slot * self.sbytes + gi * self.gbytes, self.gbytes,
-                                paths[i:i + self.group])
-                for gi, i in enumerate(range(0, len(paths), self.group))]
+        handle = [self._ex.submit(_dw.decode_group_into, self.shm.name, slot * self.sbytes + gi * self.gbytes,
+                                  self.gbytes, paths[i:i + self.group])
+                  for gi, i in enumerate(range(0, len(paths), self.group))]
+        self._writers[slot] = handle
+        return handle
 
     def upload(self, handle, slot):
         import torch
