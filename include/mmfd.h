@@ -306,10 +306,16 @@ int mmfd_mask_rows(int dtype, int64_t rows, int64_t D, void* x, int64_t ldx, con
 int mmfd_attn_fill_masked_rows(int dtype, int64_t B, int64_t H, int64_t L, int64_t Dh, const void* v, int64_t v_sb,
                                int64_t v_st, void* o, int64_t o_sb, int64_t o_st, const int64_t* mask,
                                mmfd_stream_t stream);
-/* scatter-add the gradient of the pre-LN sum into the three tables (fp32 atomics for word). */
+/* scatter-add the gradient of the pre-LN sum into the three tables (modeling_bert.py BertEmbeddings:
+   word[id] += row, pos[t] += row, type[tt] += row), deterministically: the word rows are stably
+   radix-sorted by id and each id's rows summed in row order by one writer; the type table reduces
+   fixed row slabs in order. workspace >= mmfd_embed_bwd_workspace_bytes(B, L, D); ids < 2^32,
+   B*L < 2^31. dword / dpos / dtype_emb may each be NULL (that table is skipped). */
+int64_t mmfd_embed_bwd_workspace_bytes(int64_t B, int64_t L, int64_t D);
 int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
                    const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos,
-                   float* dtype_emb, int64_t padding_idx, mmfd_stream_t stream);
+                   float* dtype_emb, int64_t padding_idx, void* workspace, int64_t workspace_bytes,
+                   mmfd_stream_t stream);
 /* key-padding mask (int64 0/1) -> additive bias (0 or `neg`, HF uses finfo(float32).min) */
 int mmfd_mask_to_bias(int64_t n, const int64_t* mask, float* out, float neg, mmfd_stream_t stream);
 

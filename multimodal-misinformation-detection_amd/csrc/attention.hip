@@ -36,7 +36,8 @@ struct AttnP {
   const float* key_bias;
   const float* rel_bias; int64_t rb_sb, rb_mod;
   const float* cos_ls; float cos_max_log;  // Swinv2 cosine attention (REL forward only)
-  float p; uint32_t thr; float keep_scale;
+  float p; uint32_t thr16; float keep_scale;
+  int64_t kp;  // key pairs per query row, ceil(Lk / 2): attention dropout hashes one index per pair
   const uint64_t* seed; uint64_t salt;
   const void* dout; int64_t do_sb, do_st;
   void* dq; int64_t dq_sb, dq_st;
@@ -141,6 +142,37 @@ __device__ __forceinline__ void x6_put4(const AttnP& p, float* dst, const float 
   *reinterpret_cast<float4*>(dst) = v;
 }
 __device__ __forceinline__ uint32_t hash_c1(uint32_t key, uint32_t idx_c1) { return mmfd_mix32(key ^ idx_c1); }
+
+// Attention dropout draws ONE 32-bit hash per key pair: element (row, k) of the [B*H*Lq][Lk] score
+// matrix (row = (b*H + h)*Lq + q) uses h = mmfd_hash_k(key, row * kp + k / 2), kp = ceil(Lk / 2),
+// and is kept when its 16-bit half (low for even k, high for odd k) is >= thr16 = round(p * 65536)
+// (p = 0.1: thr16 = 6554, a keep probability within 6e-6 of 0.9). oracle/dropout_hash.py
+// attn_keep_mask restates it. A lane holding 4 consecutive keys (forward, dQ) hashes twice where it
+// hashed four times; a lane holding one key of 4 queries (dK/dV) hashes 2 of the 4 pairs and takes
+// the other 2 from its neighbour lane (the pair partner key).
+__device__ __forceinline__ bool pair_keep(uint32_t h, int odd, uint32_t thr16) {
+  return (odd ? (h >> 16) : (h & 0xffffu)) >= thr16;
+}
+__device__ __forceinline__ uint32_t attn_hash64(uint32_t hkey, const AttnP& p, int64_t row, int64_t key) {
+  return mmfd_hash_k(hkey, (uint64_t)row * (uint64_t)p.kp + (uint64_t)(key >> 1));
+}
+// keep factors (keep_scale or 0) of 4 consecutive keys starting at an even key, from the pair hashes
+// h0 (keys 0, 1) and h1 (keys 2, 3)
+__device__ __forceinline__ void keep4_pairs(uint32_t h0, uint32_t h1, const AttnP& p, float (&z)[4]) {
+  z[0] = pair_keep(h0, 0, p.thr16) ? p.keep_scale : 0.f;
+  z[1] = pair_keep(h0, 1, p.thr16) ? p.keep_scale : 0.f;
+  z[2] = pair_keep(h1, 0, p.thr16) ? p.keep_scale : 0.f;
+  z[3] = pair_keep(h1, 1, p.thr16) ? p.keep_scale : 0.f;
+}
+// one key per lane, 4 query rows r: this lane hashed rows (odd ? 2 : 0) -> ha and (odd ? 3 : 1) -> hb
+// of its key pair; the partner lane (lane ^ 1, the pair's other key) hashed the other two rows. All
+// 64 lanes must be active.
+__device__ __forceinline__ void keep4_col(uint32_t ha, uint32_t hb, int odd, const AttnP& p, float (&z)[4]) {
+  const uint32_t xa = __shfl_xor(ha, 1, 64), xb = __shfl_xor(hb, 1, 64);
+  const uint32_t h[4] = {odd ? xa : ha, odd ? xb : hb, odd ? ha : xa, odd ? hb : xb};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) z[r] = pair_keep(h[r], odd, p.thr16) ? p.keep_scale : 0.f;
+}
 
 template <typename T, int D>
 struct AT {
@@ -346,8 +378,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP p) {
         float pe = e;
         if (p.p > 0.f) {
           const int64_t key = k0 + ks * 16 + 4 * g + r;
-          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
-          pe = (hsh < p.thr) ? 0.f : e * p.keep_scale;
+          const uint32_t hsh = attn_hash64(hkey, p, bh * p.Lq + myq, key);
+          pe = pair_keep(hsh, (int)(key & 1), p.thr16) ? e * p.keep_scale : 0.f;
         }
         s[ks][r] = pe;
       }
@@ -477,8 +509,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnP p) {
         }
         float z = 1.f;
         if (p.p > 0.f) {
-          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + q) * p.Lk + mykey));
-          z = (hsh < p.thr) ? 0.f : p.keep_scale;
+          const uint32_t hsh = attn_hash64(hkey, p, bh * p.Lq + q, mykey);
+          z = pair_keep(hsh, (int)(mykey & 1), p.thr16) ? p.keep_scale : 0.f;
         }
         pd[qs][r] = pr * z;
         ds[qs][r] = pr * (dp[r] * z - s_delta[lq]);
@@ -574,8 +606,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnP p) {
         }
         float z = 1.f;
         if (p.p > 0.f) {
-          const uint32_t hsh = mmfd_hash_k(hkey, (uint64_t)((bh * p.Lq + myq) * p.Lk + key));
-          z = (hsh < p.thr) ? 0.f : p.keep_scale;
+          const uint32_t hsh = attn_hash64(hkey, p, bh * p.Lq + myq, key);
+          z = pair_keep(hsh, (int)(key & 1), p.thr16) ? p.keep_scale : 0.f;
         }
         ds[ks][r] = pr * (dp[r] * z - dlt);
       }
@@ -834,8 +866,8 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
     if constexpr (sizeof(T) == 2) {
       if (cosine) cos_norm_q<D>(qf, qmult);
     }
-    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);  // dropout index base of this query row
-    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    const uint64_t hrow = (uint64_t)(bh * p.Lq + myq) * (uint64_t)p.kp;  // pair-index base of this query row
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(2 * g)) * HASH_C1;
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[C::DT];
@@ -934,18 +966,16 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 && !REL ? 4 : 1) at
           s[ks][r] = e;
         }
         if (drop) {  // one uniform branch per subtile (none in the fixed modes)
+          float z[4];
           if (p.idx32) {
-            const uint32_t c = rowc1 + (uint32_t)(k0 + ks * 16) * HASH_C1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              s[ks][r] = (hash_c1(hkey, c + (uint32_t)r * HASH_C1) < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
+            const uint32_t c = rowc1 + (uint32_t)((k0 + ks * 16) >> 1) * HASH_C1;
+            keep4_pairs(hash_c1(hkey, c), hash_c1(hkey, c + HASH_C1), p, z);
           } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t hsh = mmfd_hash_k(hkey, hrow + (uint64_t)(k0 + ks * 16 + 4 * g + r));
-              s[ks][r] = (hsh < p.thr) ? 0.f : s[ks][r] * p.keep_scale;
-            }
+            const uint64_t pi = hrow + (uint64_t)((k0 + ks * 16 + 4 * g) >> 1);
+            keep4_pairs(mmfd_hash_k(hkey, pi), mmfd_hash_k(hkey, pi + 1), p, z);
           }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[ks][r] *= z[r];
         }
       }
       if (MODE == 0 && p.p > 0.f && p.dm) {
@@ -1088,7 +1118,8 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
     }
     // -inf for padded keys -> P = 0 (mode 1: their dK / dV rows are computed but never stored)
     const float kb2 = MODE == 1 ? 0.f : kbias[mykey];
-    const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
+    const uint64_t hcol = (uint64_t)(bh * p.Lq) * (uint64_t)p.kp + (uint64_t)(mykey >> 1);  // pair index, query 0
+    const int kodd = (int)(mykey & 1);
     const float* relcol = REL ? p.rel_bias + rb_off(p, b) + h * p.Lq * p.Lk + (mykey < p.Lk ? mykey : 0) : nullptr;
     f32x4 dkv[2 * C::DT];  // dV (even) and dK (odd) of each 16-wide D subtile
 #pragma unroll
@@ -1144,15 +1175,12 @@ __global__ void __launch_bounds__(NTH) attn_dkdv_v2_kernel(AttnP p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) z[r] = ((col[(qs * 16 + 4 * g + r) * p.dmw] >> sh) & 1u) ? p.keep_scale : 0.f;
           } else if (p.idx32) {
-            const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
-            const uint32_t c = ((uint32_t)hcol + (uint32_t)(qs * 16 + 4 * g) * (uint32_t)p.Lk) * HASH_C1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) z[r] = (hash_c1(hkey, c + (uint32_t)r * lkc1) < p.thr) ? 0.f : p.keep_scale;
+            const uint32_t kpc1 = (uint32_t)p.kp * HASH_C1;
+            const uint32_t c = ((uint32_t)hcol + (uint32_t)(qs * 16 + 4 * g + 2 * kodd) * (uint32_t)p.kp) * HASH_C1;
+            keep4_col(hash_c1(hkey, c), hash_c1(hkey, c + kpc1), kodd, p, z);
           } else {
-            uint64_t idx = hcol + (uint64_t)(qs * 16 + 4 * g) * (uint64_t)p.Lk;
-#pragma unroll
-            for (int r = 0; r < 4; ++r, idx += (uint64_t)p.Lk)
-              z[r] = (mmfd_hash_k(hkey, idx) < p.thr) ? 0.f : p.keep_scale;
+            const uint64_t idx = hcol + (uint64_t)(qs * 16 + 4 * g + 2 * kodd) * (uint64_t)p.kp;
+            keep4_col(mmfd_hash_k(hkey, idx), mmfd_hash_k(hkey, idx + (uint64_t)p.kp), kodd, p, z);
           }
         }
 #pragma unroll
@@ -1275,7 +1303,7 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
       dlt = myq < p.Lq ? ds : 0.f;
       if (g == 0 && myq < p.Lq) p.delta[bh * p.Lq + myq] = ds;
     }
-    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
+    const uint64_t hrow = (uint64_t)(bh * p.Lq + myq) * (uint64_t)p.kp;  // pair-index base of this query row
     const float* relrow = REL ? p.rel_bias + rb_off(p, b) + (h * p.Lq + (myq < p.Lq ? myq : 0)) * p.Lk : nullptr;
     const uint32_t* dmrow = MODE == 0 && p.dm ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
     f32x4 dq[C::DT];
@@ -1340,14 +1368,11 @@ __global__ void __launch_bounds__(V2_THREADS, sizeof(T) == 2 ? 4 : 1) attn_dq_v2
 #pragma unroll
             for (int r = 0; r < 4; ++r) z[r] = ((kw >> ((ks & 1) * 16 + 4 * g + r)) & 1u) ? p.keep_scale : 0.f;
           } else if (p.idx32) {
-            const uint32_t c = ((uint32_t)hrow + (uint32_t)(ks * 16 + 4 * g)) * HASH_C1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              z[r] = (hash_c1(hkey, c + (uint32_t)r * HASH_C1) < p.thr) ? 0.f : p.keep_scale;
+            const uint32_t c = ((uint32_t)hrow + (uint32_t)(ks * 8 + 2 * g)) * HASH_C1;
+            keep4_pairs(hash_c1(hkey, c), hash_c1(hkey, c + HASH_C1), p, z);
           } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              z[r] = (mmfd_hash_k(hkey, hrow + (uint64_t)(ks * 16 + 4 * g + r)) < p.thr) ? 0.f : p.keep_scale;
+            const uint64_t pi = hrow + (uint64_t)(ks * 8 + 2 * g);
+            keep4_pairs(mmfd_hash_k(hkey, pi), mmfd_hash_k(hkey, pi + 1), p, z);
           }
         }
 #pragma unroll
@@ -1625,8 +1650,8 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
   const int nchk = nfc + ((lk16 & 63) ? 1 : 0);    // + the padded tail chunk
   auto qrun = [&](int qbk, const uint4 (&qf)[3][KCH], int c0, int c1, f32x4 (&o)[DT], float& m, float& lsum) {
     const int64_t q0 = (int64_t)qbk * 16, myq = q0 + li;
-    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
-    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    const uint64_t hrow = (uint64_t)(bh * p.Lq + myq) * (uint64_t)p.kp;  // pair-index base of this query row
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(2 * g)) * HASH_C1;
     auto chunk = [&](int k0, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-key subtiles present (4 but in the last chunk)
       constexpr int NC = (NS + 1) / 2;           // 32-key chunks of P V
@@ -1681,16 +1706,19 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_fwd_x6_kernel(AttnP p) {
         }
       }
       if constexpr (DROP) {
-        const uint32_t cc = rowc1 + (uint32_t)k0 * HASH_C1;
+        const uint32_t cc = rowc1 + (uint32_t)(k0 >> 1) * HASH_C1;
         uint32_t kbits = 0;
 #pragma unroll
-        for (int ks = 0; ks < NS; ++ks)
+        for (int ks = 0; ks < NS; ++ks) {
+          const uint32_t h0 = hash_c1(hkey, cc + (uint32_t)(ks * 8) * HASH_C1);
+          const uint32_t h1 = hash_c1(hkey, cc + (uint32_t)(ks * 8 + 1) * HASH_C1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const bool kp = hash_c1(hkey, cc + (uint32_t)(ks * 16 + r) * HASH_C1) >= p.thr;
+            const bool kp = pair_keep(r < 2 ? h0 : h1, r & 1, p.thr16);
             s[ks][r] = kp ? s[ks][r] * p.keep_scale : 0.f;
             kbits |= (uint32_t)kp << (ks * 4 + r);
           }
+        }
         if (p.dm) dm_write64(p, bh, myq, k0, g, kbits);  // the backward kernels read it
       }
       lsum = lsum * alpha + rs;
@@ -1860,9 +1888,10 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
     x6_row_split<KCH>(kf, kr);
     x6_row_split<KCH>(vf, vr);
     const float kb2 = kbias[mykey];  // -inf for padded keys -> P = 0
-    const uint64_t hcol = (uint64_t)(bh * p.Lq * p.Lk + mykey);
-    const uint32_t lkc1 = (uint32_t)p.Lk * HASH_C1;
-    const uint32_t colc1 = (uint32_t)hcol * HASH_C1 + (uint32_t)(4 * g) * lkc1;
+    const uint64_t hcol = (uint64_t)(bh * p.Lq) * (uint64_t)p.kp + (uint64_t)(mykey >> 1);  // pair index, query 0
+    const int kodd = (int)(mykey & 1);
+    const uint32_t kpc1 = (uint32_t)p.kp * HASH_C1;
+    const uint32_t colc1 = (uint32_t)hcol * HASH_C1 + (uint32_t)(4 * g + 2 * kodd) * kpc1;
     auto chunk = [&](int qc, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-query subtiles of this 32-query chunk
       f32x4 sd[4];  // S (even) and dP (odd) per subtile
@@ -1903,12 +1932,10 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dkdv_x6_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
       if constexpr (DROP == 1) {  // the element index advances by Lk per query
 #pragma unroll
-        for (int h2 = 0; h2 < NS; ++h2)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t e = colc1 + (uint32_t)((2 * qc + h2) * 16 + r) * lkc1;
-            z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
-          }
+        for (int h2 = 0; h2 < NS; ++h2) {
+          const uint32_t e = colc1 + (uint32_t)((2 * qc + h2) * 16) * kpc1;
+          keep4_col(hash_c1(hkey, e), hash_c1(hkey, e + kpc1), kodd, p, z[h2]);
+        }
       } else if constexpr (DROP == 2) {  // bit mykey of the query rows' words (LDS broadcast reads)
         const uint32_t* col = s_dm + (mykey >> 5);
         const int sh = (int)(mykey & 31);
@@ -2096,8 +2123,8 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
     dsum += __shfl_xor(dsum, 32, 64);
     const float dlt = myq < p.Lq ? dsum : 0.f;
     if (wdelta && g == 0 && myq < p.Lq) p.delta[bh * p.Lq + myq] = dsum;
-    const uint64_t hrow = (uint64_t)((bh * p.Lq + myq) * p.Lk);
-    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(4 * g)) * HASH_C1;
+    const uint64_t hrow = (uint64_t)(bh * p.Lq + myq) * (uint64_t)p.kp;  // pair-index base of this query row
+    const uint32_t rowc1 = ((uint32_t)hrow + (uint32_t)(2 * g)) * HASH_C1;
     const uint32_t* dmrow = DROP == 2 ? dm_row(p, bh, myq < p.Lq ? myq : 0) : nullptr;
     auto chunk = [&](int kc2, auto nsc) {
       constexpr int NS = decltype(nsc)::value;  // 16-key subtiles of this 32-key chunk
@@ -2137,12 +2164,10 @@ __global__ void __launch_bounds__(V2_THREADS, 1) attn_dq_x6_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) z[h2][r] = 1.f;
       if constexpr (DROP == 1) {
 #pragma unroll
-        for (int h2 = 0; h2 < NS; ++h2)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t e = rowc1 + (uint32_t)((2 * kc2 + h2) * 16 + r) * HASH_C1;
-            z[h2][r] = (hash_c1(hkey, e) < p.thr) ? 0.f : p.keep_scale;
-          }
+        for (int h2 = 0; h2 < NS; ++h2) {
+          const uint32_t e = rowc1 + (uint32_t)((2 * kc2 + h2) * 8) * HASH_C1;
+          keep4_pairs(hash_c1(hkey, e), hash_c1(hkey, e + HASH_C1), p, z[h2]);
+        }
       } else if constexpr (DROP == 2) {
 #pragma unroll
         for (int h2 = 0; h2 < NS; ++h2)
@@ -2350,7 +2375,7 @@ int fill(const mmfd_attn_args& a, AttnP& p, bool bwd) {
   p.lse = a.lse; p.key_bias = a.key_bias; p.rel_bias = a.rel_bias; p.rb_sb = a.rel_bias ? a.rel_bias_sb : 0;
   p.rb_mod = a.rel_bias ? a.rel_bias_mod : 0;
   p.cos_ls = a.cos_logit_scale; p.cos_max_log = a.cos_max_log;
-  p.p = a.dropout_p > 0.f ? a.dropout_p : 0.f; p.thr = mmfd_drop_threshold(p.p);
+  p.p = a.dropout_p > 0.f ? a.dropout_p : 0.f; p.thr16 = mmfd_drop_threshold16(p.p); p.kp = (a.Lk + 1) / 2;
   p.keep_scale = 1.0f / (1.0f - p.p); p.seed = a.seed; p.salt = a.salt;
   p.dout = a.dout; p.do_sb = a.do_sb; p.do_st = a.do_st;
   p.dq = a.dq; p.dq_sb = a.dq_sb; p.dq_st = a.dq_st;
@@ -2382,9 +2407,12 @@ __global__ void dm_fill_kernel(AttnP p) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = i / p.dmw, w = i - row * p.dmw;  // row = bh * Lq + q
     uint32_t bits = 0;
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < 32; j += 2) {  // one hash per key pair (k even, k + 1)
       const int64_t k = w * 32 + j;
-      if (k < p.Lk && mmfd_hash_k(hkey, (uint64_t)(row * p.Lk + k)) >= p.thr) bits |= 1u << j;
+      if (k >= p.Lk) break;
+      const uint32_t hsh = attn_hash64(hkey, p, row, k);
+      if (pair_keep(hsh, 0, p.thr16)) bits |= 1u << j;
+      if (k + 1 < p.Lk && pair_keep(hsh, 1, p.thr16)) bits |= 1u << (j + 1);
     }
     p.dm[i] = bits;
   }

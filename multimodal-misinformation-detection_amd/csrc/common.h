@@ -109,6 +109,12 @@ __host__ __device__ __forceinline__ uint32_t mmfd_hash_k(uint32_t key, uint64_t 
 __host__ __device__ __forceinline__ uint32_t mmfd_hash(uint64_t seed, uint64_t salt, uint64_t idx) {
   return mmfd_hash_k(mmfd_hash_key(seed, salt), idx);
 }
+// 16-bit threshold of the attention kernels' pair hashes (attention.hip pair_keep): keep <=> the
+// element's 16-bit half >= thr16 = round(p * 65536); 65536 drops everything
+__host__ __device__ __forceinline__ uint32_t mmfd_drop_threshold16(float p) {
+  const double t = (double)p * 65536.0 + 0.5;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
+}
 // threshold so that keep <=> hash >= thr, i.e. P(drop) = p
 __host__ __device__ __forceinline__ uint32_t mmfd_drop_threshold(float p) {
   double t = (double)p * 4294967296.0;

@@ -1,0 +1,173 @@
+// BERT embedding backward: the gradient of the pre-LayerNorm sum (word + position + token type,
+// modeling_bert.py BertEmbeddings.forward) scattered into the three tables — deterministically.
+//
+// The word table is a scatter-add over repeated token ids. Since round 5 it is no longer done with
+// fp32 atomics (whose order, and so the last bits of the result, changed from run to run): the
+// token rows are stably radix-sorted by id (hipCUB), and one wavefront per distinct id sums that
+// id's rows in row order and adds the sum to its table row — the only writer of that row. The
+// token-type table (two rows) sums fixed row slabs into workspace partials and reduces the slabs in
+// slab order; the position table sums over the batch in batch order. Same inputs, same bits —
+// which the graph-captured data-parallel step's self-check (mmfd.dp, tests/test_dp_gpu.py) relies on.
+#include "common.h"
+#include <algorithm>
+#include <hipcub/device/device_radix_sort.hpp>
+
+namespace {
+constexpr int kTypeSlabs = 256;
+
+inline unsigned gridn(int64_t n, int per) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, 16384));
+}
+inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+// keys = token ids (as u32: ids are table rows, < 2^32), values = row numbers
+__global__ void embed_sort_prep_kernel(int64_t rows, const int64_t* __restrict__ ids, uint32_t* __restrict__ keys,
+                                       int32_t* __restrict__ vals) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    keys[r] = (uint32_t)ids[r];
+    vals[r] = (int32_t)r;
+  }
+}
+
+// one wavefront per sorted position; the wave at the first position of an id's run sums the run's
+// rows (in row order: the sort is stable) 8 columns per lane at a time and adds the sum to the row
+template <typename T>
+__global__ void embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
+                                         const int32_t* __restrict__ vals, const T* __restrict__ dsum,
+                                         float* __restrict__ dword, int64_t padding_idx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows) return;
+  const uint32_t key = keys[i];
+  if (i > 0 && keys[i - 1] == key) return;
+  if ((int64_t)key == padding_idx) return;
+  int64_t end = i + 1;
+  while (end < rows && keys[end] == key) ++end;
+  float* out = dword + (int64_t)key * D;
+  for (int64_t d0 = 0; d0 < D; d0 += 512) {
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+    for (int64_t j = i; j < end; ++j) {
+      const T* src = dsum + (int64_t)vals[j] * D + d0 + lane;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (d0 + lane + 64 * c < D) acc[c] += to_f32(src[64 * c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (d0 + lane + 64 * c < D) out[d0 + lane + 64 * c] += acc[c];
+  }
+}
+
+// dpos[t][d] += sum_b dsum[b][t][d] (batch order)
+template <typename T>
+__global__ void embed_pos_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dsum, float* __restrict__ dpos) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L * D; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t b = 0; b < B; ++b) s += to_f32(dsum[b * L * D + i]);
+    dpos[i] += s;
+  }
+}
+
+// token types 0/1: block (x = 256 columns, y = row slab) writes its slab's two column sums to
+// part[slab][type][d]; embed_type_reduce_kernel adds the slabs in slab order
+template <typename T>
+__global__ void embed_type_part_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ tts, const T* __restrict__ dsum,
+                                       float* __restrict__ part) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = std::min<int64_t>(rows, r0 + per);
+  float s0 = 0.f, s1 = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float g = to_f32(dsum[r * D + d]);
+    if (tts && tts[r] == 1) s1 += g; else s0 += g;
+  }
+  part[((int64_t)blockIdx.y * 2) * D + d] = s0;
+  part[((int64_t)blockIdx.y * 2 + 1) * D + d] = s1;
+}
+__global__ void embed_type_reduce_kernel(int64_t D, int slabs, const float* __restrict__ part, float* __restrict__ dtype_emb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over 2*D
+  if (i >= 2 * D) return;
+  const int64_t t = i / D, d = i % D;
+  float s = 0.f;
+  for (int k = 0; k < slabs; ++k) s += part[((int64_t)k * 2 + t) * D + d];
+  dtype_emb[i] += s;
+}
+
+struct EmbedWs {
+  int64_t keys0, keys1, vals0, vals1, sort_tmp, sort_tmp_bytes, part, total;
+};
+hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
+  size_t tmp = 0;
+  hipcub::DoubleBuffer<uint32_t> k(nullptr, nullptr);
+  hipcub::DoubleBuffer<int32_t> v(nullptr, nullptr);
+  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, v, (int)rows, 0, 32, (hipStream_t)0);
+  int64_t o = 0;
+  w.keys0 = o; o += align256(rows * 4);
+  w.keys1 = o; o += align256(rows * 4);
+  w.vals0 = o; o += align256(rows * 4);
+  w.vals1 = o; o += align256(rows * 4);
+  w.sort_tmp = o; w.sort_tmp_bytes = (int64_t)tmp; o += align256((int64_t)tmp);
+  w.part = o; o += align256((int64_t)kTypeSlabs * 2 * D * 4);
+  w.total = o;
+  return e;
+}
+int type_slabs(int64_t rows) { return (int)std::min<int64_t>(kTypeSlabs, std::max<int64_t>(1, rows / 128)); }
+}  // namespace
+
+extern "C" int64_t mmfd_embed_bwd_workspace_bytes(int64_t B, int64_t L, int64_t D) {
+  if (B <= 0 || L <= 0 || D <= 0 || B * L > INT32_MAX) return 0;
+  EmbedWs w;
+  if (embed_ws_layout(B * L, D, w) != hipSuccess) return -1;
+  return w.total;
+}
+
+extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+                              const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos, float* dtype_emb,
+                              int64_t padding_idx, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
+  const int64_t rows = B * L;
+  if (rows == 0) return 0;
+  MMFD_CHECK_ARG(B > 0 && L > 0 && D > 0 && rows <= INT32_MAX, "embed_bwd: bad shape B=%lld L=%lld D=%lld",
+                 (long long)B, (long long)L, (long long)D);
+  MMFD_CHECK_ARG(dtype == MMFD_BF16 || dtype == MMFD_F32, "embed_bwd: dtype %d", dtype);
+  EmbedWs w;
+  if (embed_ws_layout(rows, D, w) != hipSuccess) return mmfd_set_error(MMFD_ERR_INVALID, "embed_bwd: sort size query failed");
+  MMFD_CHECK_ARG(workspace != nullptr && workspace_bytes >= w.total,
+                 "embed_bwd: workspace %lld B, needs %lld (mmfd_embed_bwd_workspace_bytes)", (long long)workspace_bytes,
+                 (long long)w.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const bool bf = dtype == MMFD_BF16;
+  if (dword) {
+    hipcub::DoubleBuffer<uint32_t> k((uint32_t*)(ws + w.keys0), (uint32_t*)(ws + w.keys1));
+    hipcub::DoubleBuffer<int32_t> v((int32_t*)(ws + w.vals0), (int32_t*)(ws + w.vals1));
+    hipLaunchKernelGGL(embed_sort_prep_kernel, dim3(gridn(rows, 256)), dim3(256), 0, s, rows, input_ids, k.Current(),
+                       v.Current());
+    size_t tmp = (size_t)w.sort_tmp_bytes;
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort_tmp, tmp, k, v, (int)rows, 0, 32, s);
+    if (e != hipSuccess) return mmfd_set_error((int)e, "embed_bwd: radix sort: %s", hipGetErrorString(e));
+    const dim3 g((unsigned)((rows + 3) / 4));
+    if (bf)
+      hipLaunchKernelGGL((embed_word_segsum_kernel<bf16>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
+                         (const bf16*)dsum, dword, padding_idx);
+    else
+      hipLaunchKernelGGL((embed_word_segsum_kernel<float>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
+                         (const float*)dsum, dword, padding_idx);
+  }
+  if (dpos) {
+    if (bf) hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dsum, dpos);
+    else hipLaunchKernelGGL((embed_pos_bwd_kernel<float>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const float*)dsum, dpos);
+  }
+  if (dtype_emb) {
+    const int slabs = type_slabs(rows);
+    float* part = (float*)(ws + w.part);
+    const dim3 gt((unsigned)((D + 255) / 256), (unsigned)slabs);
+    if (bf) hipLaunchKernelGGL((embed_type_part_kernel<bf16>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const bf16*)dsum, part);
+    else hipLaunchKernelGGL((embed_type_part_kernel<float>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const float*)dsum, part);
+    hipLaunchKernelGGL(embed_type_reduce_kernel, dim3((unsigned)((2 * D + 255) / 256)), dim3(256), 0, s, D, slabs, part, dtype_emb);
+  }
+  MMFD_CHECK_LAUNCH("embed_bwd");
+  return 0;
+}

@@ -210,42 +210,6 @@ __global__ void rel_bias_kernel(int64_t H, int64_t Lq, int64_t Lk, const int32_t
   }
 }
 
-template <typename T>
-__global__ void embed_word_bwd_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ ids, const T* __restrict__ dsum,
-                                      float* __restrict__ dword, int64_t padding_idx) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
-    const int64_t id = ids[row];
-    if (id == padding_idx) continue;
-    for (int64_t d = lane; d < D; d += 64) atomicAdd(dword + id * D + d, to_f32(dsum[row * D + d]));
-  }
-}
-// dpos[t][d] = sum_b dsum[b][t][d]; type grads per token type (0/1) via column partials
-template <typename T>
-__global__ void embed_pos_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dsum, float* __restrict__ dpos) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L * D; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int64_t b = 0; b < B; ++b) s += to_f32(dsum[b * L * D + i]);
-    dpos[i] += s;
-  }
-}
-template <typename T>
-__global__ void embed_type_bwd_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ tts, const T* __restrict__ dsum,
-                                      float* __restrict__ dtype_emb) {
-  // block = 256 columns x one row-slab; two accumulators (token types 0 and 1), fp32 atomics per block
-  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
-  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = std::min<int64_t>(rows, r0 + per);
-  float s0 = 0.f, s1 = 0.f;
-  for (int64_t r = r0; r < r1; ++r) {
-    const float g = to_f32(dsum[r * D + d]);
-    if (tts && tts[r] == 1) s1 += g; else s0 += g;
-  }
-  atomicAdd(dtype_emb + d, s0);
-  atomicAdd(dtype_emb + D + d, s1);
-}
-
 // ---------------------------------------------------------------------------------------------
 // ViT
 // ---------------------------------------------------------------------------------------------
@@ -453,28 +417,6 @@ extern "C" int mmfd_rel_bias(int64_t H, int64_t Lq, int64_t Lk, const int32_t* b
   if (n == 0) return 0;
   hipLaunchKernelGGL(rel_bias_kernel, dim3(gridn(n, 256)), dim3(256), 0, (hipStream_t)stream, H, Lq, Lk, bucket, table, out);
   MMFD_CHECK_LAUNCH("rel_bias");
-  return 0;
-}
-
-extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
-                              const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos, float* dtype_emb,
-                              int64_t padding_idx, mmfd_stream_t stream) {
-  const int64_t rows = B * L;
-  if (rows == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  const unsigned gw = gridn(rows, 4);
-  const int slabs = (int)std::min<int64_t>(256, std::max<int64_t>(1, rows / 128));
-  dim3 gt((unsigned)((D + 255) / 256), (unsigned)slabs);
-  if (dtype == MMFD_BF16) {
-    if (dword) hipLaunchKernelGGL((embed_word_bwd_kernel<bf16>), dim3(gw), dim3(256), 0, s, rows, D, input_ids, (const bf16*)dsum, dword, padding_idx);
-    if (dpos) hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dsum, dpos);
-    if (dtype_emb) hipLaunchKernelGGL((embed_type_bwd_kernel<bf16>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const bf16*)dsum, dtype_emb);
-  } else {
-    if (dword) hipLaunchKernelGGL((embed_word_bwd_kernel<float>), dim3(gw), dim3(256), 0, s, rows, D, input_ids, (const float*)dsum, dword, padding_idx);
-    if (dpos) hipLaunchKernelGGL((embed_pos_bwd_kernel<float>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const float*)dsum, dpos);
-    if (dtype_emb) hipLaunchKernelGGL((embed_type_bwd_kernel<float>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const float*)dsum, dtype_emb);
-  }
-  MMFD_CHECK_LAUNCH("embed_bwd");
   return 0;
 }
 

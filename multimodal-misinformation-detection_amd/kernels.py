@@ -146,7 +146,8 @@ SIGNATURES = {
     "mmfd_xent_fwd_bwd": (_I, [_I, _I64, _I64, _VP, _VP, _VP, _I64, _VP, _I, _VP, _VP, _VP]),
     "mmfd_embed_ln_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
                                _F, _VP, _U64, _VP]),
-    "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP]),
+    "mmfd_embed_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "mmfd_mask_to_bias": (_I, [_I64, _VP, _VP, _F, _VP]),
     "mmfd_embed_ln_fwd_ex": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
                                   _F, _VP, _U64, _VP]),
@@ -864,10 +865,16 @@ def global_avgpool(x, N, HW, C):
 
 
 def embed_bwd(ids, tts, dsum, dword, dpos, dtype_emb, padding_idx=-1):
+    """deterministic embedding-table gradients (csrc/embed_bwd.hip): sort-by-id word scatter-add"""
     B, L = ids.shape
     D = dsum.shape[-1]
+    nws = lib().mmfd_embed_bwd_workspace_bytes(B, L, D)
+    if nws < 0:
+        raise RuntimeError("mmfd_embed_bwd_workspace_bytes failed")
+    ws = torch.empty(max(nws, 1), device=dsum.device, dtype=torch.uint8)
     _check(lib().mmfd_embed_bwd(dtype_code(dsum.dtype), B, L, D, _ptr(ids), _ptr(tts) if tts is not None else None,
-                                _ptr(dsum), _ptr(dword), _ptr(dpos), _ptr(dtype_emb), int(padding_idx), _stream()),
+                                _ptr(dsum), _ptr(dword), _ptr(dpos), _ptr(dtype_emb), int(padding_idx), _ptr(ws), nws,
+                                _stream()),
            "mmfd_embed_bwd")
 
 

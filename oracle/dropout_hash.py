@@ -62,6 +62,30 @@ def salt_of(name: str) -> int:
     return (zlib.crc32(b) << 32) | zlib.crc32(b[::-1] + b"mmfd")
 
 
+def drop_threshold16(p: float) -> int:
+    """attention kernels' 16-bit threshold (common.h mmfd_drop_threshold16): round(p * 65536)"""
+    t = float(np.float32(p)) * 65536.0 + 0.5
+    return 65536 if t >= 65536.0 else int(t)
+
+
+def attn_keep_mask(seed: int, salt: int, shape, p: float, rows=None):
+    """Keep-mask of attention probabilities [B, H, Lq, Lk] as the attention kernels draw it
+    (multimodal-misinformation-detection_amd/csrc/attention.hip pair_keep): ONE hash per key pair,
+    h = hash(row * kp + k // 2) with row = (b*H + h)*Lq + q and kp = ceil(Lk / 2); element (row, k) is
+    kept when its 16-bit half (low for even k, high for odd k) >= round(p * 65536). `rows`: the
+    whole-batch indices of the tensor's batch rows (chunked oracle steps; default arange(B))."""
+    B, H, Lq, Lk = (int(x) for x in shape)
+    rows = np.arange(B, dtype=np.uint64) if rows is None else np.asarray(rows, dtype=np.uint64)
+    kp = np.uint64((Lk + 1) // 2)
+    r = ((rows[:, None, None] * np.uint64(H) + np.arange(H, dtype=np.uint64)[None, :, None]) * np.uint64(Lq)
+         + np.arange(Lq, dtype=np.uint64)[None, None, :])
+    k = np.arange(Lk, dtype=np.uint64)
+    pidx = r[..., None] * kp + (k >> np.uint64(1))[None, None, None, :]
+    h = dropout_hash(seed, salt, pidx.reshape(-1)).reshape(B, H, Lq, Lk).astype(np.int64)
+    half = np.where((k & np.uint64(1)).astype(bool)[None, None, None, :], h >> 16, h & 0xFFFF)
+    return half >= drop_threshold16(p)
+
+
 def keep_mask_rows(seed: int, salt: int, shape, p: float, rows):
     """Keep-mask of a batch-major contiguous tensor of `shape` that holds the batch rows `rows` of a
     larger whole batch: element e of batch row r has the whole-batch flat index
@@ -77,7 +101,8 @@ def keep_mask_rows(seed: int, salt: int, shape, p: float, rows):
 
 
 class Drop:
-    """`drop(site, x)` callback for the oracle: applies exactly the HIP kernels' mask. With `rows`
+    """`drop(site, x)` callback for the oracle: applies exactly the HIP kernels' mask (sites ending in
+    ".attn" — attention probabilities — with attn_keep_mask, every other site with keep_mask). With `rows`
     (the whole-batch row indices of this call's batch rows, see keep_mask_rows) a chunk of a larger
     batch gets the masks the whole batch gets at those rows: oracle.train_step.chunked_loss_grads
     binds one per chunk for the encoders (stacked claim|evidence rows [s:e] and [B+s:B+e]) and one
@@ -91,7 +116,9 @@ class Drop:
 
     def __call__(self, site, x):
         import torch
-        if self.rows is None:
+        if site.endswith(".attn"):  # attention probabilities [B, H, Lq, Lk]: the pair-hash mask
+            keep = attn_keep_mask(self.seed, salt_of(site), tuple(x.shape), self.p, self.rows)
+        elif self.rows is None:
             keep = keep_mask(self.seed, salt_of(site), tuple(x.shape), self.p)
         else:
             keep = keep_mask_rows(self.seed, salt_of(site), tuple(x.shape), self.p, self.rows)

@@ -201,15 +201,11 @@ def _worker_nccl(port, q):
                         diffs.append((si, n, "grad None mismatch"))
                     elif p.grad is not None and not torch.equal(p.grad, q_.grad):
                         diffs.append((si, n, float((p.grad - q_.grad).abs().max() / p.grad.abs().max())))
-            # bit for bit, except the word-embedding gradient: its scatter-add (misc.hip
-            # embed_word_bwd_kernel) accumulates repeated token ids with fp32 atomics, whose order
-            # is not fixed between runs — 1-ulp differences there (and in those embedding rows after
-            # AdamW) are not a DP effect
-            emb = "embeddings.word_embeddings.weight"
-            same_grad = all(d[1] == emb and isinstance(d[2], float) and d[2] < 1e-6 for d in diffs)
-            same_par = all(torch.equal(p, q_) or (n == emb and float((p - q_).abs().max()) < 1e-6)
-                           for n, p, q_ in zip(names, a.params, b.params))
-            same_loss = bool(torch.equal(la, lb)) or float((la - lb).abs().max()) < 1e-6
+            # bit for bit: every gradient kernel is deterministic (the embedding tables' scatter-add
+            # sorts rows by id since round 5, csrc/embed_bwd.hip)
+            same_grad = not diffs
+            same_par = all(torch.equal(p, q_) for p, q_ in zip(a.params, b.params))
+            same_loss = bool(torch.equal(la, lb))
             out[name] = (same_loss, same_grad, same_par, dict(a.dp.last_buckets), diffs[:12])
         out["backend"] = dist.get_backend()
         q.put(out)
@@ -226,8 +222,8 @@ def test_dp_nccl_world1_overlapped_allreduce():
     stream bucket packing, the async all_reduce on RCCL's stream and finish()'s wait + unpack run for
     two eager steps, tiny (many 50 KB buckets) and full size (default 32 MB buckets); a one-rank
     all-reduce is an identity, so losses, gradients and updated parameters equal the trainer
-    without DP bit for bit (the word-embedding gradient, accumulated with fp32 atomics, within
-    1e-6 of its max)."""
+    without DP bit for bit (every gradient kernel is deterministic: the embedding tables' scatter-add
+    sorts rows by id, csrc/embed_bwd.hip)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
@@ -271,7 +267,6 @@ def _worker_nccl_graph(port, q):
             a.capture(static_a, warmup=1)
             b.capture(static_b, warmup=1)
             names = [n for m in (a.text_encoder, a.image_encoder, a.head) for n, _ in m.named_parameters()]
-            emb = "embeddings.word_embeddings.weight"
             ok = []
             for bt in batches[1:]:
                 la = a.replay({k: v.cuda() for k, v in bt.items()}).clone()
@@ -279,11 +274,14 @@ def _worker_nccl_graph(port, q):
                 torch.cuda.synchronize()
                 bad = []
                 for n, p, q_ in zip(names, a.params, b.params):
-                    tol = 1e-6 if n == emb else 0.0  # fp32 atomics in the word-embedding scatter-add
-                    for x, y in ((p.grad, q_.grad), (p.detach(), q_.detach())):
-                        if (x is None) != (y is None) or (x is not None and
-                                                          float((x - y).abs().max()) > tol * max(1.0, float(y.abs().max()))):
-                            bad.append(n)
+                    tol = 0.0  # bit for bit (deterministic kernels, csrc/embed_bwd.hip)
+                    for what, x, y in (("grad", p.grad, q_.grad), ("param", p.detach(), q_.detach())):
+                        if (x is None) != (y is None):
+                            bad.append((n, what, "None"))
+                        elif x is not None:
+                            d = float((x - y).abs().max())
+                            if d > tol * max(1.0, float(y.abs().max())):
+                                bad.append((n, what, d, float(y.abs().max())))
                 ok.append((float((la - lb).abs().max()), bad[:8]))
             buckets = dict(a.dp.last_buckets)
             # the bench's self-check of a captured DP step (one more replay, then the cross-rank
@@ -304,8 +302,8 @@ def test_dp_nccl_world1_graph_captured_step():
     """the data-parallel step captured as ONE HIP graph — forward, backward with the
     per-stream bucket packs and the RCCL all_reduce kernels, finish()'s wait + unpack, AdamW — on
     ProcessGroupNCCL (RCCL) with one rank. Replayed on new batches it must equal the plain captured
-    step (no DP) in losses, gradients and updated parameters, bit for bit (the word-embedding
-    gradient, accumulated with fp32 atomics, within 1e-6), tiny with 50 KB buckets and full size
+    step (no DP) in losses, gradients and updated parameters, bit for bit (deterministic kernels:
+    csrc/embed_bwd.hip), tiny with 50 KB buckets and full size
     with the default 32 MB buckets, dropout on. Since round 5 the captured all-reduces run on the DP
     object's dedicated capture group in the thread-local capture mode (no quiesce sleep before the
     capture; mmfd.dp), and the bench's cross-rank self-check (verify_capture) runs on it."""

@@ -11,7 +11,7 @@ import torch
 
 import mmfd
 from mmfd import kernels as K
-from oracle.dropout_hash import keep_mask
+from oracle.dropout_hash import attn_keep_mask, keep_mask
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -246,7 +246,7 @@ def test_attention_fwd_bwd(dtype, case, masked, p):
     salt = K.salt_of("test.attn")
     keep = None
     if p > 0:
-        keep = torch.from_numpy(keep_mask(77, salt, (B, H, Lq, Lk), p)).double()
+        keep = torch.from_numpy(attn_keep_mask(77, salt, (B, H, Lq, Lk), p)).double()
     qd, kvd, dod = q.to(DEV), kv.to(DEV), dout.to(DEV)
     o, lse = K.attn_fwd(qd, kvd[..., : H * D], kvd[..., H * D:], H, key_bias=kb, dropout_p=p, seed=seed, salt=salt)
     dq, dk, dv = K.attn_bwd(qd, kvd[..., : H * D], kvd[..., H * D:], o, lse, dod, H, key_bias=kb, dropout_p=p,
@@ -287,7 +287,7 @@ def test_attention_fp32_split_operands_error_matches_fp32_mfma(case):
         kb = K.mask_to_bias(mask.to(DEV))
         kb_cpu = kb.cpu()
     seed, salt = K.Seed(78), K.salt_of("test.attn.x6")
-    keep = torch.from_numpy(keep_mask(78, salt, (B, H, Lq, Lk), p)).double() if p > 0 else None
+    keep = torch.from_numpy(attn_keep_mask(78, salt, (B, H, Lq, Lk), p)).double() if p > 0 else None
     qd, kvd, dod = q.to(DEV), kv.to(DEV), dout.to(DEV)
     outs = {}
     old = K.set_fp32_attn_mode("split")
@@ -780,7 +780,7 @@ def _pack_keep_bits(keep, Lk):
 def test_attention_dropout_keep_bitmask(dtype, B, H, L, D):
     """the forward writes the dropout keep-mask once as a bitmask
     (mmfd_attn_args.drop_mask) and the backward reads it instead of re-hashing. The words equal the
-    oracle's counter-hash mask (oracle/dropout_hash.keep_mask) bit for bit on every valid key, and
+    oracle's counter-hash mask (oracle/dropout_hash.attn_keep_mask: one hash per key pair) bit for bit on every valid key, and
     output, lse, dQ, dK and dV are bit-identical with and without the mask — BERT's shape (the
     split-operand / bf16 resident kernels, mask staged in LDS by dK/dV), the head's D = 32 at
     L = 197 (fp32: dK/dV has no LDS left for the mask and re-hashes), and L = 300 (the streaming
@@ -805,9 +805,47 @@ def test_attention_dropout_keep_bitmask(dtype, B, H, L, D):
     for a, b in zip(res[False][:5], res[True][:5]):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
     words = res[True][5].cpu().numpy().view(np.uint32).reshape(B, H * L, -1)
-    want = _pack_keep_bits(keep_mask(91, salt, (B, H, L, L), p), L).reshape(B, H * L, -1)
+    want = _pack_keep_bits(attn_keep_mask(91, salt, (B, H, L, L), p), L).reshape(B, H * L, -1)
     # compared on the keys a query attends to (the bf16 resident forward records the mask from P,
     # whose masked-out keys are 0 whatever the hash: their backward P is 0 as well)
     for b in range(B):
         valid = _pack_keep_bits(np.arange(L)[None, None, None, :] < int(lens[b]), L).reshape(-1)
         assert np.array_equal(words[b] & valid, want[b] & valid), b
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,D", [(8, 64, 768), (3, 37, 100), (1, 1, 64)])
+def test_embed_bwd_deterministic_scatter_add(dtype, B, L, D):
+    """csrc/embed_bwd.hip: the embedding tables' gradients (word: sort rows by id, one writer per id;
+    type: ordered slab partials; position: batch order) equal an fp64 index_add of the same rows, add
+    into what the tables held, skip padding rows, and repeat bit for bit (heavily repeated ids)."""
+    g = torch.Generator().manual_seed(B * 1000 + L)
+    V = 50
+    ids = torch.randint(0, V, (B, L), generator=g).cuda()
+    tts = torch.randint(0, 2, (B, L), generator=g).cuda()
+    dsum = (torch.randn(B, L, D, generator=g)).to(dtype).cuda()
+    base = [torch.randn(V, D, generator=g).cuda(), torch.randn(L, D, generator=g).cuda(),
+            torch.randn(2, D, generator=g).cuda()]
+    outs = []
+    for _ in range(2):
+        dword, dpos, dtyp = (t.clone() for t in base)
+        K.embed_bwd(ids, tts, dsum, dword, dpos, dtyp, padding_idx=0)
+        torch.cuda.synchronize()
+        outs.append((dword, dpos, dtyp))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    x = dsum.double().reshape(B * L, D).cpu()
+    i = ids.reshape(-1).cpu()
+    keep = i != 0
+    rw = base[0].double().cpu().index_add(0, i[keep], x[keep])
+    rp = base[1].double().cpu() + x.reshape(B, L, D).sum(0)
+    rt = base[2].double().cpu().index_add(0, tts.reshape(-1).cpu(), x)
+    for got, ref in zip(outs[0], (rw, rp, rt)):
+        err = (got.double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+    # NULL tables are skipped
+    dword = base[0].clone()
+    K.embed_bwd(ids, None, dsum, dword, None, None, padding_idx=-1)
+    torch.cuda.synchronize()
+    rw = base[0].double().cpu().index_add(0, i, x)
+    assert (dword.double().cpu() - rw).abs().max().item() <= 1e-5 * max(1.0, rw.abs().max().item())

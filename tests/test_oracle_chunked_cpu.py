@@ -49,3 +49,21 @@ def test_chunked_dropout_step_equals_whole_batch_step():
     # the mapping matters: chunk-local masks give another loss
     local = chunked_loss_grads(*states, batch, chunk=1, drop=_ChunkLocal(7, 0.1), drop_head=_ChunkLocal(8, 0.1), **kw)
     assert abs(local[0].item() - whole[0].item()) > 1e-4
+
+
+def test_attn_keep_mask_pairs_rows_and_rate():
+    """attention masks (one hash per key pair, 16-bit halves): whole-batch rows map like keep_mask_rows,
+    odd Lk pads the last pair, the keep rate is 1 - p within sampling error, and the two halves of a
+    pair are not correlated"""
+    from oracle.dropout_hash import attn_keep_mask, drop_threshold16
+    assert drop_threshold16(0.1) == 6554 and drop_threshold16(0.0) == 0 and drop_threshold16(1.0) == 65536
+    full = attn_keep_mask(5, salt_of("a.attn"), (5, 3, 7, 13), 0.1)
+    rows = np.array([3, 0, 4])
+    assert (attn_keep_mask(5, salt_of("a.attn"), (3, 3, 7, 13), 0.1, rows) == full[rows]).all()
+    big = attn_keep_mask(11, salt_of("b.attn"), (4, 8, 64, 128), 0.1)
+    rate = big.mean()
+    assert abs(rate - 0.9) < 0.004, rate
+    even, odd = big[..., 0::2].astype(np.float64), big[..., 1::2].astype(np.float64)
+    corr = ((even - even.mean()) * (odd - odd.mean())).mean() / (even.std() * odd.std())
+    assert abs(corr) < 0.01, corr
+    assert not attn_keep_mask(1, 2, (1, 1, 4, 6), 1.0).any() and attn_keep_mask(1, 2, (1, 1, 4, 6), 0.0).all()
