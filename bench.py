@@ -912,6 +912,11 @@ def train_leg(args, dev, world, rank, precision):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # optimizer steps this trainer has taken when the timed region ends (the last one's loss is
+    # final_loss): capture's eager warm-up + warm-up replays + timed replays, or eager warm-up + timed
+    opt_steps = (max(1, args.warmup) + args.warmup + args.steps) if graphed else (args.warmup + args.steps)
+    if graphed and world > 1:
+        opt_steps += 1  # capture_dp_step's verifying replay
     t0 = time.perf_counter()
     if graphed:
         for _ in range(args.steps):
@@ -993,7 +998,7 @@ def train_leg(args, dev, world, rank, precision):
                              "achieved = 2MNK per launch / launch time")
         roof["bf16_mfma_view"] = {"achieved": round(6 * achieved, 1), "peak": PEAK_TFLOPS["bf16"],
                                   "note": "the same launches as executed bf16 MFMA FLOPs (6 x 2MNK) over the bf16 peak"}
-    return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
+    return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "loss_exact": loss_val, "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
             "first_loss": None if first_loss is None else [round(v, 6) for v in first_loss.double().cpu().tolist()],
             "dp_check": dp_check,
             "launch": (("one HIP graph per step (captured fwd + bwd + AdamW" + (" + RCCL gradient all-reduce)" if world > 1
@@ -1001,7 +1006,8 @@ def train_leg(args, dev, world, rank, precision):
                        + ("; text / image encoders on two streams" if tr_conc else "")
                        + "; GEMM times from 2 eager probe steps after the timed region, encoders serialized"),
             "gemm_tf": round(gemm_tf, 1), "step_tflops": pairs / world * GFLOP_PER_PAIR[args.mode] / 1e3,
-            "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1), "memory": mem}
+            "step_peak": step_peak(precision), "roofline": roof, "peak_memory_gb": round(peak_gb, 1), "memory": mem,
+            "opt_steps": opt_steps, "world": world}
 
 
 def first_step_parity(args, res):
@@ -1023,8 +1029,20 @@ def first_step_parity(args, res):
     out = {"max_abs_err": float(np.abs(got - want).max()), "got": res["first_loss"],
            "oracle": [round(float(v), 6) for v in want], "bound": 1e-3,
            "fixture": "tests/golden/config3_bs256_p01.npz (oracle, chunked whole-batch dropout masks)"}
+    traj_path = os.path.join(ROOT, "tests", "golden", "config3_bs256_p01_traj.npz")
+    if traj is None and os.path.exists(traj_path):
+        with np.load(traj_path) as z:
+            traj = z["loss_steps"][:, 0].tolist()
     if traj is not None and len(traj) > 1:
         out["oracle_loss_trajectory"] = [round(float(v), 6) for v in traj]
+        # final_loss reproduced: the oracle's loss after the same number of optimizer steps on the
+        # same batch (one rank: rank r > 0 trains on another seed)
+        n = res.get("opt_steps")
+        if n and res.get("world", 1) == 1 and n <= len(traj):
+            got = float(res.get("loss_exact", res["loss"]))
+            out["final_loss"] = {"step": n, "got": round(got, 6), "oracle": round(float(traj[n - 1]), 6),
+                                 "abs_err": abs(got - float(traj[n - 1])), "bound": 5e-3,
+                                 "fixture": "tests/golden/config3_bs256_p01_traj.npz"}
     return out
 
 

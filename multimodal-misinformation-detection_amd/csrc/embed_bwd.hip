@@ -3,8 +3,9 @@
 //
 // The word table is a scatter-add over repeated token ids. Since round 5 it is no longer done with
 // fp32 atomics (whose order, and so the last bits of the result, changed from run to run): the
-// token rows are stably radix-sorted by id (hipCUB), and one wavefront per distinct id sums that
-// id's rows in row order and adds the sum to its table row — the only writer of that row. The
+// token rows are stably radix-sorted by id (hipCUB), each id's rows are summed in row order in
+// pieces of at most kSegChunk sorted rows, and the pieces are added in order by a single writer
+// per table row. The
 // token-type table (two rows) sums fixed row slabs into workspace partials and reduces the slabs in
 // slab order; the position table sums over the batch in batch order. Same inputs, same bits —
 // which the graph-captured data-parallel step's self-check (mmfd.dp, tests/test_dp_gpu.py) relies on.
@@ -29,34 +30,111 @@ __global__ void embed_sort_prep_kernel(int64_t rows, const int64_t* __restrict__
   }
 }
 
-// one wavefront per sorted position; the wave at the first position of an id's run sums the run's
-// rows (in row order: the sort is stable) 8 columns per lane at a time and adds the sum to the row
+// The sorted positions are cut into chunks of kSegChunk; one wavefront per chunk walks its runs of
+// equal ids and sums each run's rows in row order (the sort is stable). A run wholly inside the chunk
+// is added to its table row directly (its only writer); the pieces of a run that crosses chunk
+// boundaries go to per-chunk partials — part_last[c] for the piece a run starts with at the end
+// of chunk c, part_first[c] for the piece that continues a run from chunk c - 1 — and
+// embed_word_join_kernel adds them in chunk order. A repeated id ([CLS], [SEP], "the") costs
+// ceil(count / kSegChunk) parallel pieces and one short ordered join, not a serial walk.
+constexpr int kSegChunk = 32;
+
+template <typename T>
+__device__ __forceinline__ void seg_sum_rows(const T* __restrict__ dsum, const int32_t* __restrict__ vals, int64_t s,
+                                             int64_t e, int64_t D, int lane, int64_t d0, float (&acc)[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+#pragma unroll 4
+  for (int64_t j = s; j < e; ++j) {
+    const T* src = dsum + (int64_t)vals[j] * D + d0 + lane;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (d0 + lane + 64 * c < D) acc[c] += to_f32(src[64 * c]);
+  }
+}
+
 template <typename T>
 __global__ void embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
                                          const int32_t* __restrict__ vals, const T* __restrict__ dsum,
-                                         float* __restrict__ dword, int64_t padding_idx) {
+                                         float* __restrict__ dword, float* __restrict__ part_first,
+                                         float* __restrict__ part_last, int64_t padding_idx) {
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= rows) return;
-  const uint32_t key = keys[i];
-  if (i > 0 && keys[i - 1] == key) return;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t i0 = c * kSegChunk;
+  if (i0 >= rows) return;
+  const int64_t i1 = i0 + kSegChunk < rows ? i0 + kSegChunk : rows;
+  for (int64_t s = i0; s < i1;) {
+    const uint32_t key = keys[s];
+    int64_t e = s + 1;
+    while (e < i1 && keys[e] == key) ++e;
+    const bool before = s == i0 && i0 > 0 && keys[i0 - 1] == key;
+    const bool after = e == i1 && i1 < rows && keys[i1] == key;
+    const bool pad = (int64_t)key == padding_idx;
+    if (!pad || before || after) {
+      float* dst = before ? part_first + c * D : after ? part_last + c * D : dword + (int64_t)key * D;
+      for (int64_t d0 = 0; d0 < D; d0 += 512) {
+        float acc[8];
+        seg_sum_rows<T>(dsum, vals, s, e, D, lane, d0, acc);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int64_t d = d0 + lane + 64 * q;
+          if (d < D) {
+            if (before || after) dst[d] = acc[q];
+            else dst[d] += acc[q];
+          }
+        }
+      }
+    }
+    s = e;
+  }
+}
+
+// one wavefront per chunk whose last run starts in it and crosses into the next chunk: the run's
+// pieces (part_last of this chunk, part_first of the following ones) added in chunk order
+__global__ void embed_word_join_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
+                                       const float* __restrict__ part_first, const float* __restrict__ part_last,
+                                       float* __restrict__ dword, int64_t padding_idx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t i0 = c * kSegChunk, i1 = i0 + kSegChunk;
+  if (i1 >= rows) return;  // the last chunk has no successor
+  const uint32_t key = keys[i1 - 1];
+  if (keys[i1] != key) return;
+  // the run must start inside this chunk (else an earlier chunk joins it)
+  if (keys[i0] == key && i0 > 0 && keys[i0 - 1] == key) return;
   if ((int64_t)key == padding_idx) return;
-  int64_t end = i + 1;
-  while (end < rows && keys[end] == key) ++end;
-  float* out = dword + (int64_t)key * D;
+  // the following chunks the run reaches are those that start with its id (the keys are sorted):
+  // 64 chunks tested per ballot
+  const int64_t nch = (rows + kSegChunk - 1) / kSegChunk;
+  int64_t n = 0;
+  for (;;) {
+    const int64_t cc = c + 1 + n + lane;
+    const bool in = cc < nch && keys[cc * kSegChunk] == key;
+    const uint64_t m = __ballot(in);
+    const int run = m == ~0ull ? 64 : __builtin_ctzll(~m);  // leading chunks of the run (m has no gaps)
+    n += run;
+    if (run < 64) break;
+  }
   for (int64_t d0 = 0; d0 < D; d0 += 512) {
     float acc[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-    for (int64_t j = i; j < end; ++j) {
-      const T* src = dsum + (int64_t)vals[j] * D + d0 + lane;
+    for (int q = 0; q < 8; ++q) {
+      const int64_t d = d0 + lane + 64 * q;
+      acc[q] = d < D ? part_last[c * D + d] : 0.f;
+    }
+#pragma unroll 4
+    for (int64_t cc = c + 1; cc <= c + n; ++cc) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (d0 + lane + 64 * c < D) acc[c] += to_f32(src[64 * c]);
+      for (int q = 0; q < 8; ++q) {
+        const int64_t d = d0 + lane + 64 * q;
+        if (d < D) acc[q] += part_first[cc * D + d];
+      }
     }
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (d0 + lane + 64 * c < D) out[d0 + lane + 64 * c] += acc[c];
+    for (int q = 0; q < 8; ++q) {
+      const int64_t d = d0 + lane + 64 * q;
+      if (d < D) dword[(int64_t)key * D + d] += acc[q];
+    }
   }
 }
 
@@ -65,6 +143,7 @@ template <typename T>
 __global__ void embed_pos_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* __restrict__ dsum, float* __restrict__ dpos) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L * D; i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
+#pragma unroll 8
     for (int64_t b = 0; b < B; ++b) s += to_f32(dsum[b * L * D + i]);
     dpos[i] += s;
   }
@@ -92,12 +171,13 @@ __global__ void embed_type_reduce_kernel(int64_t D, int slabs, const float* __re
   if (i >= 2 * D) return;
   const int64_t t = i / D, d = i % D;
   float s = 0.f;
+#pragma unroll 16
   for (int k = 0; k < slabs; ++k) s += part[((int64_t)k * 2 + t) * D + d];
   dtype_emb[i] += s;
 }
 
 struct EmbedWs {
-  int64_t keys0, keys1, vals0, vals1, sort_tmp, sort_tmp_bytes, part, total;
+  int64_t keys0, keys1, vals0, vals1, sort_tmp, sort_tmp_bytes, part, seg_first, seg_last, total;
 };
 hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
   size_t tmp = 0;
@@ -111,6 +191,9 @@ hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
   w.vals1 = o; o += align256(rows * 4);
   w.sort_tmp = o; w.sort_tmp_bytes = (int64_t)tmp; o += align256((int64_t)tmp);
   w.part = o; o += align256((int64_t)kTypeSlabs * 2 * D * 4);
+  const int64_t nch = (rows + kSegChunk - 1) / kSegChunk;
+  w.seg_first = o; o += align256(nch * D * 4);
+  w.seg_last = o; o += align256(nch * D * 4);
   w.total = o;
   return e;
 }
@@ -148,13 +231,17 @@ extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const 
     size_t tmp = (size_t)w.sort_tmp_bytes;
     const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort_tmp, tmp, k, v, (int)rows, 0, 32, s);
     if (e != hipSuccess) return mmfd_set_error((int)e, "embed_bwd: radix sort: %s", hipGetErrorString(e));
-    const dim3 g((unsigned)((rows + 3) / 4));
+    const int64_t nch = (rows + kSegChunk - 1) / kSegChunk;
+    const dim3 g((unsigned)((nch + 3) / 4));
+    float* pf = (float*)(ws + w.seg_first);
+    float* pl = (float*)(ws + w.seg_last);
     if (bf)
       hipLaunchKernelGGL((embed_word_segsum_kernel<bf16>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
-                         (const bf16*)dsum, dword, padding_idx);
+                         (const bf16*)dsum, dword, pf, pl, padding_idx);
     else
       hipLaunchKernelGGL((embed_word_segsum_kernel<float>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
-                         (const float*)dsum, dword, padding_idx);
+                         (const float*)dsum, dword, pf, pl, padding_idx);
+    hipLaunchKernelGGL(embed_word_join_kernel, g, dim3(256), 0, s, rows, D, k.Current(), pf, pl, dword, padding_idx);
   }
   if (dpos) {
     if (bf) hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dsum, dpos);

@@ -220,7 +220,8 @@ def _attn_ref(q, k, v, H, scale, key_bias=None, keep=None, p=0.0):
 ATTN_CASES = [(2, 4, 128, 128, 64), (2, 8, 197, 197, 32), (3, 2, 13, 29, 64), (2, 8, 128, 197, 32),
               (1, 12, 70, 70, 64), (2, 4, 21, 33, 8), (2, 2, 40, 40, 16), (1, 3, 65, 130, 48),
               (1, 2, 260, 300, 64), (2, 16, 256, 256, 64),  # L > 256: streaming backward kernels
-              (1, 2, 512, 512, 64)]  # bf16 forward keeps up to 512 keys resident
+              (1, 2, 512, 512, 64),  # bf16 forward keeps up to 512 keys resident
+              (2, 4, 197, 197, 64), (1, 2, 208, 208, 64)]  # 13 query blocks: the last one split over two waves
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -814,13 +815,14 @@ def test_attention_dropout_keep_bitmask(dtype, B, H, L, D):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,L,D", [(8, 64, 768), (3, 37, 100), (1, 1, 64)])
-def test_embed_bwd_deterministic_scatter_add(dtype, B, L, D):
+@pytest.mark.parametrize("B,L,D,V", [(8, 64, 768, 50), (3, 37, 100, 50), (1, 1, 64, 50), (16, 128, 200, 3),
+                                     (4, 100, 768, 2), (40, 128, 64, 2), (40, 128, 64, 1)])
+def test_embed_bwd_deterministic_scatter_add(dtype, B, L, D, V):
     """csrc/embed_bwd.hip: the embedding tables' gradients (word: sort rows by id, one writer per id;
     type: ordered slab partials; position: batch order) equal an fp64 index_add of the same rows, add
-    into what the tables held, skip padding rows, and repeat bit for bit (heavily repeated ids)."""
+    into what the tables held, skip padding rows, and repeat bit for bit (heavily repeated ids; V = 2-3:
+    runs of hundreds of rows across many 32-row pieces, the padding id's run included)."""
     g = torch.Generator().manual_seed(B * 1000 + L)
-    V = 50
     ids = torch.randint(0, V, (B, L), generator=g).cuda()
     tts = torch.randint(0, 2, (B, L), generator=g).cuda()
     dsum = (torch.randn(B, L, D, generator=g)).to(dtype).cuda()

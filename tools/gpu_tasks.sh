@@ -42,7 +42,7 @@ for task in "$@"; do
   eval "set -- $task"
   t=$1; shift
   case $t in
-    tests) run 900 "tests${LIB:+_$LIB}.log" "$(lib_env) python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread ${*:-tests}" ;;
+    tests) args=$(printf '%q ' "$@"); run 900 "tests${LIB:+_$LIB}.log" "$(lib_env) python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread ${args:-tests}" ;;
     smoke) run 300 smoke.log "$(lib_env) python -c 'import __graft_entry__ as g; g.smoke()'" ;;
     bench) run 400 bench.log "$(lib_env) python bench.py $*" ;;
     ab)
