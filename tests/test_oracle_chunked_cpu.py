@@ -67,3 +67,18 @@ def test_attn_keep_mask_pairs_rows_and_rate():
     corr = ((even - even.mean()) * (odd - odd.mean())).mean() / (even.std() * odd.std())
     assert abs(corr) < 0.01, corr
     assert not attn_keep_mask(1, 2, (1, 1, 4, 6), 1.0).any() and attn_keep_mask(1, 2, (1, 1, 4, 6), 0.0).all()
+
+
+def test_bench_trajectory_fixture_starts_at_the_one_step_fixture():
+    """tests/golden/config3_bs256_p01_traj.npz (30 oracle AdamW steps of the bench recipe, the
+    reference for bench.py's final_loss) begins with the one-step fixture's loss vector and records
+    the recipe it was made from"""
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    one = np.load(os.path.join(g, "config3_bs256_p01.npz"))
+    traj = np.load(os.path.join(g, "config3_bs256_p01_traj.npz"))
+    assert str(traj["recipe"]) == "bench" == str(one["recipe"])
+    steps = traj["loss_steps"]
+    assert steps.shape == (30, 5) and np.isfinite(steps).all()
+    assert np.abs(steps[0] - one["loss"]).max() <= 1e-12
+    assert steps[-1, 0] < steps[0, 0]  # the fixed batch is being fitted
