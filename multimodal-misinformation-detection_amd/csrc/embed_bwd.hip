@@ -14,7 +14,7 @@
 #include <hipcub/device/device_radix_sort.hpp>
 
 namespace {
-constexpr int kTypeSlabs = 256;
+constexpr int kTypeSlabs = 1024;
 
 inline unsigned gridn(int64_t n, int per) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, 16384));
@@ -39,29 +39,16 @@ __global__ void embed_sort_prep_kernel(int64_t rows, const int64_t* __restrict__
 // ceil(count / kSegChunk) parallel pieces and one short ordered join, not a serial walk.
 constexpr int kSegChunk = 32;
 
+// one 256-thread block per chunk (thread t owns columns t + 256 u): 32 rows' loads per thread in
+// flight across the unrolled row loop, 4 waves per chunk
 template <typename T>
-__device__ __forceinline__ void seg_sum_rows(const T* __restrict__ dsum, const int32_t* __restrict__ vals, int64_t s,
-                                             int64_t e, int64_t D, int lane, int64_t d0, float (&acc)[8]) {
-#pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-#pragma unroll 4
-  for (int64_t j = s; j < e; ++j) {
-    const T* src = dsum + (int64_t)vals[j] * D + d0 + lane;
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (d0 + lane + 64 * c < D) acc[c] += to_f32(src[64 * c]);
-  }
-}
-
-template <typename T>
-__global__ void embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
-                                         const int32_t* __restrict__ vals, const T* __restrict__ dsum,
-                                         float* __restrict__ dword, float* __restrict__ part_first,
-                                         float* __restrict__ part_last, int64_t padding_idx) {
-  const int lane = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ void __launch_bounds__(256) embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
+                                                                const int32_t* __restrict__ vals, const T* __restrict__ dsum,
+                                                                float* __restrict__ dword, float* __restrict__ part_first,
+                                                                float* __restrict__ part_last, int64_t padding_idx) {
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
   const int64_t i0 = c * kSegChunk;
-  if (i0 >= rows) return;
   const int64_t i1 = i0 + kSegChunk < rows ? i0 + kSegChunk : rows;
   for (int64_t s = i0; s < i1;) {
     const uint32_t key = keys[s];
@@ -72,15 +59,21 @@ __global__ void embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t
     const bool pad = (int64_t)key == padding_idx;
     if (!pad || before || after) {
       float* dst = before ? part_first + c * D : after ? part_last + c * D : dword + (int64_t)key * D;
-      for (int64_t d0 = 0; d0 < D; d0 += 512) {
-        float acc[8];
-        seg_sum_rows<T>(dsum, vals, s, e, D, lane, d0, acc);
+      for (int64_t d0 = 0; d0 < D; d0 += 1024) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int64_t j = s; j < e; ++j) {
+          const T* src = dsum + (int64_t)vals[j] * D + d0 + t;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int64_t d = d0 + lane + 64 * q;
+          for (int u = 0; u < 4; ++u)
+            if (d0 + t + 256 * u < D) acc[u] += to_f32(src[256 * u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t d = d0 + t + 256 * u;
           if (d < D) {
-            if (before || after) dst[d] = acc[q];
-            else dst[d] += acc[q];
+            if (before || after) dst[d] = acc[u];
+            else dst[d] += acc[u];
           }
         }
       }
@@ -89,13 +82,14 @@ __global__ void embed_word_segsum_kernel(int64_t rows, int64_t D, const uint32_t
   }
 }
 
-// one wavefront per chunk whose last run starts in it and crosses into the next chunk: the run's
-// pieces (part_last of this chunk, part_first of the following ones) added in chunk order
-__global__ void embed_word_join_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
-                                       const float* __restrict__ part_first, const float* __restrict__ part_last,
-                                       float* __restrict__ dword, int64_t padding_idx) {
-  const int lane = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+// one block per chunk whose last run starts in it and crosses into the next chunk: the run's pieces
+// (part_last of this chunk, part_first of the following ones) added in chunk order
+__global__ void __launch_bounds__(256) embed_word_join_kernel(int64_t rows, int64_t D, const uint32_t* __restrict__ keys,
+                                                              const float* __restrict__ part_first,
+                                                              const float* __restrict__ part_last,
+                                                              float* __restrict__ dword, int64_t padding_idx) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int64_t c = blockIdx.x;
   const int64_t i0 = c * kSegChunk, i1 = i0 + kSegChunk;
   if (i1 >= rows) return;  // the last chunk has no successor
   const uint32_t key = keys[i1 - 1];
@@ -104,7 +98,7 @@ __global__ void embed_word_join_kernel(int64_t rows, int64_t D, const uint32_t* 
   if (keys[i0] == key && i0 > 0 && keys[i0 - 1] == key) return;
   if ((int64_t)key == padding_idx) return;
   // the following chunks the run reaches are those that start with its id (the keys are sorted):
-  // 64 chunks tested per ballot
+  // 64 chunks tested per ballot (every wave of the block computes the same count)
   const int64_t nch = (rows + kSegChunk - 1) / kSegChunk;
   int64_t n = 0;
   for (;;) {
@@ -115,26 +109,11 @@ __global__ void embed_word_join_kernel(int64_t rows, int64_t D, const uint32_t* 
     n += run;
     if (run < 64) break;
   }
-  for (int64_t d0 = 0; d0 < D; d0 += 512) {
-    float acc[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int64_t d = d0 + lane + 64 * q;
-      acc[q] = d < D ? part_last[c * D + d] : 0.f;
-    }
-#pragma unroll 4
-    for (int64_t cc = c + 1; cc <= c + n; ++cc) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int64_t d = d0 + lane + 64 * q;
-        if (d < D) acc[q] += part_first[cc * D + d];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int64_t d = d0 + lane + 64 * q;
-      if (d < D) dword[(int64_t)key * D + d] += acc[q];
-    }
+  for (int64_t d = t; d < D; d += 256) {
+    float acc = part_last[c * D + d];
+#pragma unroll 8
+    for (int64_t cc = c + 1; cc <= c + n; ++cc) acc += part_first[cc * D + d];
+    dword[(int64_t)key * D + d] += acc;
   }
 }
 
@@ -150,7 +129,8 @@ __global__ void embed_pos_bwd_kernel(int64_t B, int64_t L, int64_t D, const T* _
 }
 
 // token types 0/1: block (x = 256 columns, y = row slab) writes its slab's two column sums to
-// part[slab][type][d]; embed_type_reduce_kernel adds the slabs in slab order
+// part[slab][type][d]; embed_type_reduce_kernel adds them in a fixed order (16 runs of slabs, each
+// in slab order, then the runs in order)
 template <typename T>
 __global__ void embed_type_part_kernel(int64_t rows, int64_t D, const int64_t* __restrict__ tts, const T* __restrict__ dsum,
                                        float* __restrict__ part) {
@@ -159,6 +139,7 @@ __global__ void embed_type_part_kernel(int64_t rows, int64_t D, const int64_t* _
   const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
   const int64_t r0 = (int64_t)blockIdx.y * per, r1 = std::min<int64_t>(rows, r0 + per);
   float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
   for (int64_t r = r0; r < r1; ++r) {
     const float g = to_f32(dsum[r * D + d]);
     if (tts && tts[r] == 1) s1 += g; else s0 += g;
@@ -166,14 +147,29 @@ __global__ void embed_type_part_kernel(int64_t rows, int64_t D, const int64_t* _
   part[((int64_t)blockIdx.y * 2) * D + d] = s0;
   part[((int64_t)blockIdx.y * 2 + 1) * D + d] = s1;
 }
-__global__ void embed_type_reduce_kernel(int64_t D, int slabs, const float* __restrict__ part, float* __restrict__ dtype_emb) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over 2*D
-  if (i >= 2 * D) return;
-  const int64_t t = i / D, d = i % D;
+// 64 outputs (of the 2 x D) per 1,024-thread block: wave w sums slabs [w S/16, (w+1) S/16) in order,
+// wave 0 adds the 16 wave sums in wave order
+__global__ void __launch_bounds__(1024) embed_type_reduce_kernel(int64_t D, int slabs, const float* __restrict__ part,
+                                                                 float* __restrict__ dtype_emb) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;  // output index over 2 * D
+  const bool ok = i < 2 * D;
+  const int64_t t = ok ? i / D : 0, d = ok ? i % D : 0;
+  const int per = (slabs + 15) / 16, k0 = w * per, k1 = min(slabs, k0 + per);
   float s = 0.f;
-#pragma unroll 16
-  for (int k = 0; k < slabs; ++k) s += part[((int64_t)k * 2 + t) * D + d];
-  dtype_emb[i] += s;
+  if (ok) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += part[((int64_t)k * 2 + t) * D + d];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && ok) {
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) r += red[q][lane];
+    dtype_emb[i] += r;
+  }
 }
 
 struct EmbedWs {
@@ -197,7 +193,7 @@ hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
   w.total = o;
   return e;
 }
-int type_slabs(int64_t rows) { return (int)std::min<int64_t>(kTypeSlabs, std::max<int64_t>(1, rows / 128)); }
+int type_slabs(int64_t rows) { return (int)std::min<int64_t>(kTypeSlabs, std::max<int64_t>(1, rows / 64)); }
 }  // namespace
 
 extern "C" int64_t mmfd_embed_bwd_workspace_bytes(int64_t B, int64_t L, int64_t D) {
@@ -231,8 +227,7 @@ extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const 
     size_t tmp = (size_t)w.sort_tmp_bytes;
     const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort_tmp, tmp, k, v, (int)rows, 0, 32, s);
     if (e != hipSuccess) return mmfd_set_error((int)e, "embed_bwd: radix sort: %s", hipGetErrorString(e));
-    const int64_t nch = (rows + kSegChunk - 1) / kSegChunk;
-    const dim3 g((unsigned)((nch + 3) / 4));
+    const dim3 g((unsigned)((rows + kSegChunk - 1) / kSegChunk));
     float* pf = (float*)(ws + w.seg_first);
     float* pl = (float*)(ws + w.seg_last);
     if (bf)
@@ -253,7 +248,7 @@ extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const 
     const dim3 gt((unsigned)((D + 255) / 256), (unsigned)slabs);
     if (bf) hipLaunchKernelGGL((embed_type_part_kernel<bf16>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const bf16*)dsum, part);
     else hipLaunchKernelGGL((embed_type_part_kernel<float>), gt, dim3(256), 0, s, rows, D, token_type_ids, (const float*)dsum, part);
-    hipLaunchKernelGGL(embed_type_reduce_kernel, dim3((unsigned)((2 * D + 255) / 256)), dim3(256), 0, s, D, slabs, part, dtype_emb);
+    hipLaunchKernelGGL(embed_type_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64)), dim3(1024), 0, s, D, slabs, part, dtype_emb);
   }
   MMFD_CHECK_LAUNCH("embed_bwd");
   return 0;
