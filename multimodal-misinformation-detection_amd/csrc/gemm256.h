@@ -7,6 +7,16 @@
 
 namespace {
 
+// G8_PF: the bf16 loop's kc = 0 fragment reads one phase ahead, inside the previous phase's MFMA
+// block (see the main loop): 2 = interleaved one read per 2-4 products (default, +3.9 % over the
+// encoder GEMM shapes, same-box A/B), 1 = as one burst after the kc = 0 products (-2.7 %), 0 = off
+#ifndef G8_PF
+#define G8_PF 2
+#endif
+#ifndef G8_PF_XI
+#define G8_PF_XI 4
+#endif
+
 // PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
 // prefetched for all of a thread's rows before the accumulators are staged (see the epilogue)
 
@@ -93,7 +103,9 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0);
     if (nk > 1) {
       issue(0, 1); issue(2, 1); issue(3, 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      // (G8_PF: all of K-tile 0, A-h1 included — the leading row reads it in X(0)'s MFMA block)
+      if (G8_PF) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -123,7 +135,104 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   auto rs_on = [&](int t) { return !X6 || ((X6_RS >> ((kt0 + t) / x6.nkt)) & 1u); };
 
   uint4 fa[4][2], fb[2][2];
-  if constexpr (PH2) {
+  if constexpr (PH2 && G8_PF) {
+    // The two-phase schedule below with each phase's kc = 0 fragments read one phase AHEAD, inside
+    // the previous phase's MFMA block right after the kc = 0 products that free their registers:
+    // X(t)'s MFMAs read A-h1(t) kc 0, Y(t)'s read A-h0 / B-h0 / B-h1 of t+1 kc 0, so each read section
+    // keeps only the kc = 1 half (X 8 reads instead of 16, Y 4 instead of 8). Landing: the lagging
+    // wave row must have landed the next phase's pieces before the barrier that opens the leading
+    // row's MFMA block, hence one counted wait before each closing barrier — vmcnt(2) after X (only
+    // X's own A-h1 refill may fly), vmcnt(6) after Y — on pieces issued a whole phase earlier.
+    uint4 fbh[2][2];
+    if (nk > 0) {
+      g8_frag_a_kc<T, TA>(fa, img(0, 0), wr, lane, 0);
+      g8_frag_b_kc<T, TB>(fb, img(0, 2), wc, lane, 0);
+      g8_frag_b_kc<T, TB>(fbh, img(0, 3), wc, lane, 0);
+    }
+    for (int t = 0; t < nk; ++t) {
+      bool rs_t = false;
+      if (do_rs) {
+        rs_t = rs_ph == tcol && rs_on(t);
+        rs_ph = rs_ph + 1 == rs_cols ? 0 : rs_ph + 1;
+      }
+      // phase X(t)
+      g8_frag_a_kc<T, TA>(fa, img(t, 0), wr, lane, 1);
+      g8_frag_b_kc<T, TB>(fb, img(t, 2), wc, lane, 1);
+      g8_frag_b_kc<T, TB>(fbh, img(t, 3), wc, lane, 1);
+      if (rs_t) rs0 += g8_rowsum<T, TA>(img(t, 0), wr, wc, lane);
+      if (t + 1 < nk) {
+        issue(1, t + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      g8_pre_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      g8_mma2_kc<T>(acc[0][0], acc[0][1], fa, fb, fbh, 0);
+      if (G8_PF == 1) __builtin_amdgcn_sched_barrier(0);
+      g8_frag_a_kc<T, TA>(fa, img(t, 1), wr, lane, 0);  // Y(t)'s A-h1, kc 0
+      if (G8_PF == 1) __builtin_amdgcn_sched_barrier(0);
+      g8_mma2_kc<T>(acc[0][0], acc[0][1], fa, fb, fbh, 1);
+      if (G8_PF == 2) {  // the 4 reads one per G8_PF_XI of the kc = 1 products
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, G8_PF_XI, 0);
+        }
+        if (G8_PF_XI < 4) __builtin_amdgcn_sched_group_barrier(0x008, 16 - 4 * G8_PF_XI, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (G8_PF == 1) {
+        if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      g8_barrier();
+      // phase Y(t)
+      g8_frag_a_kc<T, TA>(fa, img(t, 1), wr, lane, 1);
+      if (rs_t) rs1 += g8_rowsum<T, TA>(img(t, 1), wr, wc, lane);
+      if (t + 2 < nk) {
+        issue(0, t + 2); issue(2, t + 2); issue(3, t + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      g8_pre_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      g8_mma2_kc<T>(acc[1][0], acc[1][1], fa, fb, fbh, 0);
+      if (G8_PF == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) {  // X(t+1)'s kc 0
+          g8_frag_a_kc<T, TA>(fa, img(t + 1, 0), wr, lane, 0);
+          g8_frag_b_kc<T, TB>(fb, img(t + 1, 2), wc, lane, 0);
+          g8_frag_b_kc<T, TB>(fbh, img(t + 1, 3), wc, lane, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {  // straight-line: past the last K-tile the reads fetch an unused image (in bounds)
+        const int tn = t + 1 < nk ? t + 1 : t;
+        g8_frag_a_kc<T, TA>(fa, img(tn, 0), wr, lane, 0);
+        g8_frag_b_kc<T, TB>(fb, img(tn, 2), wc, lane, 0);
+        g8_frag_b_kc<T, TB>(fbh, img(tn, 3), wc, lane, 0);
+      }
+      g8_mma2_kc<T>(acc[1][0], acc[1][1], fa, fb, fbh, 1);
+      if (G8_PF == 2) {  // the 8 reads one per 2 of the kc = 1 products
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (G8_PF == 1) {
+        if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
+      g8_barrier();
+    }
+  } else if constexpr (PH2) {
     // Two phases per K-tile, 32 MFMAs each (one quadrant per phase, as fp32 below, measured 3.5 %
     // slower over the encoder shapes: twice the barrier hand-offs): X(t) = quadrants (0,0), (0,1)
     // from A-h0 and both B halves; Y(t) = quadrants (1,0), (1,1) from A-h1 with the B fragments

@@ -454,6 +454,30 @@ __device__ __forceinline__ void g8_mma2(f32x4 (&acc0)[4][2], f32x4 (&acc1)[4][2]
   __builtin_amdgcn_s_setprio(0);
 }
 
+// one k-chunk (kc) of the fragment sets / of a two-quadrant phase: the bf16 loop's kc = 0 halves are
+// read one phase ahead (G8_PF, see gemm256_kernel)
+template <typename T, int LAYOUT>
+__device__ __forceinline__ void g8_frag_a_kc(uint4 (&a)[4][2], const char* img, int wr, int lane, int kc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i][kc] = load_frag<T, LAYOUT, 128>(img, wr * 4 + i, kc, lane);
+}
+template <typename T, int LAYOUT>
+__device__ __forceinline__ void g8_frag_b_kc(uint4 (&b)[2][2], const char* img, int wc, int lane, int kc) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b[j][kc] = g8_load_b<T, LAYOUT>(img, wc, j, kc, lane);
+}
+template <typename T>
+__device__ __forceinline__ void g8_mma2_kc(f32x4 (&acc0)[4][2], f32x4 (&acc1)[4][2], const uint4 (&a)[4][2],
+                                           const uint4 (&b0)[2][2], const uint4 (&b1)[2][2], int kc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      Mma<T>::run(acc0[i][j], b0[j][kc], a[i][kc]);
+      Mma<T>::run(acc1[i][j], b1[j][kc], a[i][kc]);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ float g8_sum16b(uint4 x) {  // the elements of one 16-B chunk
   if (sizeof(T) == 4)
