@@ -7,14 +7,11 @@
 
 namespace {
 
-// G8_PF: the bf16 loop's kc = 0 fragment reads one phase ahead, inside the previous phase's MFMA
-// block (see the main loop): 2 = interleaved one read per 2-4 products (default, +3.9 % over the
-// encoder GEMM shapes, same-box A/B), 1 = as one burst after the kc = 0 products (-2.7 %), 0 = off
+// G8_PF: the bf16 loop's kc = 0 fragment reads one phase ahead, interleaved into the previous
+// phase's MFMA block (see the main loop; +3.9 % over the encoder GEMM shapes, same-box A/B;
+// profiles/r05_g8_*_ab.txt for the variants measured); 0 = the round-4 schedule
 #ifndef G8_PF
-#define G8_PF 2
-#endif
-#ifndef G8_PF_XI
-#define G8_PF_XI 4
+#define G8_PF 1
 #endif
 
 // PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
@@ -169,25 +166,17 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_pre_barrier();
       __builtin_amdgcn_s_setprio(1);
       g8_mma2_kc<T>(acc[0][0], acc[0][1], fa, fb, fbh, 0);
-      if (G8_PF == 1) __builtin_amdgcn_sched_barrier(0);
       g8_frag_a_kc<T, TA>(fa, img(t, 1), wr, lane, 0);  // Y(t)'s A-h1, kc 0
-      if (G8_PF == 1) __builtin_amdgcn_sched_barrier(0);
       g8_mma2_kc<T>(acc[0][0], acc[0][1], fa, fb, fbh, 1);
-      if (G8_PF == 2) {  // the 4 reads one per G8_PF_XI of the kc = 1 products
-        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+      // the 4 reads one per 4 of the kc = 1 products (as one burst after the kc = 0 products: -2.7 %)
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, G8_PF_XI, 0);
-        }
-        if (G8_PF_XI < 4) __builtin_amdgcn_sched_group_barrier(0x008, 16 - 4 * G8_PF_XI, 0);
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
       __builtin_amdgcn_s_setprio(0);
-      if (G8_PF == 1) {
-        if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       g8_barrier();
       // phase Y(t)
       g8_frag_a_kc<T, TA>(fa, img(t, 1), wr, lane, 1);
@@ -201,35 +190,22 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       g8_pre_barrier();
       __builtin_amdgcn_s_setprio(1);
       g8_mma2_kc<T>(acc[1][0], acc[1][1], fa, fb, fbh, 0);
-      if (G8_PF == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) {  // X(t+1)'s kc 0
-          g8_frag_a_kc<T, TA>(fa, img(t + 1, 0), wr, lane, 0);
-          g8_frag_b_kc<T, TB>(fb, img(t + 1, 2), wc, lane, 0);
-          g8_frag_b_kc<T, TB>(fbh, img(t + 1, 3), wc, lane, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {  // straight-line: past the last K-tile the reads fetch an unused image (in bounds)
+      {  // X(t+1)'s kc 0, straight-line: past the last K-tile the reads fetch an unused image (in bounds)
         const int tn = t + 1 < nk ? t + 1 : t;
         g8_frag_a_kc<T, TA>(fa, img(tn, 0), wr, lane, 0);
         g8_frag_b_kc<T, TB>(fb, img(tn, 2), wc, lane, 0);
         g8_frag_b_kc<T, TB>(fbh, img(tn, 3), wc, lane, 0);
       }
       g8_mma2_kc<T>(acc[1][0], acc[1][1], fa, fb, fbh, 1);
-      if (G8_PF == 2) {  // the 8 reads one per 2 of the kc = 1 products
-        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+      // the 8 reads one per 2 of the kc = 1 products
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       }
       __builtin_amdgcn_s_setprio(0);
-      if (G8_PF == 1) {
-        if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       g8_barrier();
     }
   } else if constexpr (PH2) {

@@ -64,7 +64,26 @@ def test_gemm_layouts(dtype, layout, shape):
     assert err <= rtol * math.sqrt(Kd) * 4 + 1e-4, err
 
 
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+@pytest.mark.parametrize("Kd", [64, 128, 192, 256, 320])
+def test_gemm_bf16_g8_ktile_counts(layout, Kd):
+    """the bf16 G8 loop at 1-5 K-tiles (round 5: each phase's kc = 0 fragments are read one phase
+    ahead, with counted waits that change at the last two K-tiles), every operand layout, ragged
+    M / N, fp32 and bf16 outputs, against fp64"""
+    M, N = 300, 520
+    ta, tb = layout[0] == "t", layout[1] == "t"
+    A = _rand(*((Kd, M) if ta else (M, Kd)), dtype=torch.bfloat16, seed=Kd + 1)
+    B = _rand(*((Kd, N) if tb else (N, Kd)), dtype=torch.bfloat16, seed=Kd + 2)
+    ref = (A.double().T if ta else A.double()) @ (B.double() if tb else B.double().T)
+    for odt in (torch.float32, torch.bfloat16):
+        out = K.gemm(A.to(DEV), B.to(DEV), trans_a=ta, trans_b=tb, out_dtype=odt)
+        torch.cuda.synchronize()
+        err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= (1e-5 if odt == torch.float32 else 8e-3), (odt, err)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_long_k(dtype):@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_long_k(dtype):
     # dW of a BERT-like layer: K (tokens) long, small output -> split-K path
     Kd, M, N = 8192, 256, 384
