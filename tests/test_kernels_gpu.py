@@ -83,7 +83,6 @@ def test_gemm_bf16_g8_ktile_counts(layout, Kd):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_splitk_long_k(dtype):@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_long_k(dtype):
     # dW of a BERT-like layer: K (tokens) long, small output -> split-K path
     Kd, M, N = 8192, 256, 384
