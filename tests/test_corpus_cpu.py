@@ -152,14 +152,27 @@ def test_sharded_text_corpus_equals_single_process(tmp_path):
     assert e1.dtype == np.float16 and np.array_equal(e1, e2)
 
 
-def test_process_pool_decode_is_bit_exact(tmp_path):
+def test_process_pool_decode_is_bit_exact(tmp_path, monkeypatch):
     """mmfd.hostdecode.DecodePool (worker processes, pixels returned in shared memory) returns exactly
     the bytes of evidence._decode (PIL open + convert("RGB")) for JPEG / PNG / grayscale / RGBA /
-    palette files, in submission order, and leaves no shared-memory block behind."""
+    palette files, in submission order, and leaves none of its shared-memory blocks behind (the
+    blocks this pool handed back are tracked by name, so tests running beside it under xdist do not
+    count)."""
+    from multiprocessing import shared_memory
+
     from PIL import Image
 
+    import mmfd.hostdecode as hd
     from mmfd.evidence import _decode
     from mmfd.hostdecode import DecodePool
+    seen = []
+
+    class _Tracked(shared_memory.SharedMemory):
+        def __init__(self, name=None, create=False, size=0):
+            super().__init__(name=name, create=create, size=size)
+            seen.append(self.name.lstrip("/"))
+
+    monkeypatch.setattr(hd.shared_memory, "SharedMemory", _Tracked)
     rng = np.random.default_rng(7)
     paths = []
     for i, (mode, ext) in enumerate([("RGB", "jpg"), ("RGB", "png"), ("L", "jpg"), ("RGBA", "png"), ("P", "png"),
@@ -172,7 +185,6 @@ def test_process_pool_decode_is_bit_exact(tmp_path):
         p = str(tmp_path / f"x{i:02d}.{ext}")
         im.save(p)
         paths.append(p)
-    shm_before = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
     pool = DecodePool(workers=3, group=4)
     try:
         h1 = pool.submit(paths[:10])
@@ -189,8 +201,9 @@ def test_process_pool_decode_is_bit_exact(tmp_path):
             pool.get(pool.submit([str(tmp_path / "missing.jpg")]))
     finally:
         pool.close()
-    if shm_before or os.path.isdir("/dev/shm"):
-        assert set(os.listdir("/dev/shm")) - shm_before == set()
+    assert len(seen) == 6  # one block per 4-path group: 3 for the first 10 paths, 3 for the last 11
+    if os.path.isdir("/dev/shm"):
+        assert set(seen) & set(os.listdir("/dev/shm")) == set()
 
 
 def test_corpus_decode_processes_equals_threads(tmp_path):
