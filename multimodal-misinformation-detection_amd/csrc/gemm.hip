@@ -604,6 +604,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
       const X6Args x6{(int)((a.K + 63) / 64), (uint32_t)xp.pa, (uint32_t)xp.pb};
       dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s, &x6, pa, pb);
     }
+  } else if (g8 && bf && cbf && !ws && mmfd_gemmx::launch_g4(a, e, splits, s)) {
   } else if (g8 && bf) { if (cbf) dispatch_g8<bf16, bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
   else if (g8) dispatch_g8<float, float>(a, e, ws, splits, tps, rs_out, rs_mode, s);
   else if (bf) { if (cbf) dispatch_layout<bf16, bf16>(a, e, ws, splits, tps, s); else dispatch_layout<bf16, float>(a, e, ws, splits, tps, s); }

@@ -441,13 +441,43 @@ def gemm(A, B, *, trans_a=False, trans_b=False, out=None, out_dtype=None, alpha=
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        probe.records.append((_probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits), 2 * M * N * K,
-                              e0, e1))
+        probe.records.append((_probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha=alpha,
+                                          residual_first=residual_first, dropout_p=dropout_p, a_rowsum=a_rowsum,
+                                          aux=aux, bias=bias), 2 * M * N * K, e0, e1))
     return out
 
 
-def _probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits):
+def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, residual_first, dropout_p, a_rowsum,
+             aux, bias):
+    """the four-wave kernel's epilogue mode for this product, or None (mirrors mmfd_gemmx::launch_g4;
+    GemmProbe bookkeeping only)"""
+    if os.environ.get("MMFD_G4", "1").startswith("0") or trans_a or trans_b or splits > 1 or a_rowsum is not None:
+        return None
+    if A.dtype != torch.bfloat16 or out.dtype != torch.bfloat16 or alpha != 1.0 or beta != 0.0:
+        return None
+    M, K = A.shape
+    N = B.shape[0]
+    if M % 256 or N % 256 or K % 64 or K < 64 or K > 1024:
+        return None
+    ts = [t for t in (A, B, out, residual, aux, bias) if t is not None]
+    if any(t.data_ptr() % 16 for t in ts) or any(_ld(t) % 8 for t in (A, B, out, residual, aux) if t is not None):
+        return None
+    if act == ACT_NONE and residual is None and dropout_p <= 0:
+        return 0
+    if act == ACT_NONE and residual is not None and not residual_first:
+        return 2 if dropout_p > 0 else 1
+    if act == ACT_GELU and residual is None and dropout_p <= 0:
+        return 3
+    return None
+
+
+def _probe_name(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha=1.0, residual_first=False,
+                dropout_p=0.0, a_rowsum=None, aux=None, bias=None):
     """the kernel instantiation mmfd_gemm picks (GemmProbe bookkeeping only)"""
+    g4 = _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, residual_first, dropout_p,
+                  a_rowsum, aux, bias)
+    if g4 is not None:
+        return f"gemm_g4_kernel<{g4}>"
     M, K = (A.shape[1], A.shape[0]) if trans_a else A.shape
     N = B.shape[1] if trans_b else B.shape[0]
     a = GemmArgs()

@@ -82,6 +82,64 @@ def test_gemm_bf16_g8_ktile_counts(layout, Kd):
         assert err <= (1e-5 if odt == torch.float32 else 8e-3), (odt, err)
 
 
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 128), (768, 2304, 768), (1024, 512, 1024),
+                                   (2048, 3072, 768)])
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_gemm_bf16_g4_forward(shape, with_bias, monkeypatch):
+    """the four-wave assembly-scheduled forward GEMM (gemm_g4.hip: bf16 -> bf16, K-contiguous
+    operands, full 256x256 tiles, bias epilogue) against fp64, and against gemm256_kernel on the same
+    inputs (MMFD_G4=0 routes the product there): both accumulate each output's K in the same order
+    of 16x16x32 MFMAs from zero and round once to bf16"""
+    M, N, Kd = shape
+    A = _rand(M, Kd, dtype=torch.bfloat16, seed=M + 7).to(DEV)
+    B = _rand(N, Kd, dtype=torch.bfloat16, seed=N + 8).to(DEV)
+    bias = _rand(N, seed=Kd + 9).to(DEV) if with_bias else None
+    ref = A.double().cpu() @ B.double().cpu().T + (bias.double().cpu() if with_bias else 0.0)
+    monkeypatch.setenv("MMFD_G4", "1")
+    g4 = K.gemm(A, B, bias=bias)
+    monkeypatch.setenv("MMFD_G4", "0")
+    g8 = K.gemm(A, B, bias=bias)
+    torch.cuda.synchronize()
+    err = (g4.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 8e-3, err
+    diff = (g4.float() - g8.float()).abs().max().item()
+    ulp = (g8.float().abs().max().item() * 2.0 ** -7)
+    assert diff <= ulp, (diff, ulp)
+
+
+@pytest.mark.parametrize("mode", ["gelu_aux", "residual", "dropout_residual"])
+def test_gemm_bf16_g4_epilogues_match_g8(mode, monkeypatch):
+    """the four-wave kernel's fused epilogues of the encoder forward Linears (FFN1: bias + GELU with
+    the pre-activation to aux; attention output / FFN2: bias [+ hashed dropout] + residual) are
+    bit-identical to gemm256_kernel's on the same inputs"""
+    M, N, Kd = 768, 1024, 768
+    A = _rand(M, Kd, dtype=torch.bfloat16, seed=51).to(DEV)
+    B = _rand(N, Kd, dtype=torch.bfloat16, seed=52).to(DEV)
+    bias = _rand(N, seed=53).to(DEV)
+    res = _rand(M, N, dtype=torch.bfloat16, seed=54).to(DEV)
+    outs = {}
+    for g4 in ("1", "0"):
+        monkeypatch.setenv("MMFD_G4", g4)
+        aux = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        if mode == "gelu_aux":
+            out = K.gemm(A, B, bias=bias, act=K.ACT_GELU, aux=aux)
+        elif mode == "residual":
+            out = K.gemm(A, B, bias=bias, residual=res)
+        else:
+            out = K.gemm(A, B, bias=bias, residual=res, dropout_p=0.1, seed=K.Seed(77, device=DEV), salt=5)
+        outs[g4] = (out, aux)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    assert torch.equal(outs["1"][1], outs["0"][1])
+    ref = A.double().cpu() @ B.double().cpu().T + bias.double().cpu()
+    if mode == "residual":
+        ref = ref + res.double().cpu()
+    if mode != "dropout_residual":
+        got = outs["1"][1] if mode == "gelu_aux" else outs["1"][0]
+        err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= 8e-3, err
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_long_k(dtype):
     # dW of a BERT-like layer: K (tokens) long, small output -> split-K path

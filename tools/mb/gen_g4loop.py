@@ -1,0 +1,283 @@
+"""Generates tools/mb/g4loop.hip: a microbenchmark of the four-wave bf16 GEMM main loop the hipBLASLt
+kernel runs (DESIGN §3 "The hipBLASLt kernel's code"), written as ONE inline-assembly block so that
+no compiler scheduling is involved:
+
+  256 threads = 4 waves (one per SIMD), each wave a 128x128 block of 8x8 16x16 MFMA tiles with the
+  256 fp32 accumulators in AGPRs (a[0:255]); 64-deep K-iterations staged in two 64-KB LDS stages,
+  each stage split into A-kc0 / A-kc1 / B-kc0 / B-kc1 regions of 16 KB (kc = 32-deep K half);
+  per iteration t and wave:
+    barrier (vmcnt(16): the kc1 regions of t landed; lgkmcnt(0): kc0 fragments of t in registers)
+    part A: 64 MFMAs on the kc0 fragments, with 16 ds_read_b128 of t's kc1 fragments and 8 LDS-DMA
+            pieces refilling the kc0 regions of stage t%2 for iteration t+2
+    barrier (vmcnt(16): the kc0 regions of t+1 landed; lgkmcnt(0): kc1 fragments in registers)
+    part B: 64 MFMAs on the kc1 fragments, with 16 ds_read_b128 of t+1's kc0 fragments and 8 pieces
+            refilling the kc1 regions of stage t%2 for t+2
+  so every DMA piece has ~1.5 iterations of lead and two barriers per iteration guard the LDS reuse.
+
+No correctness: the data is whatever the source buffer holds; the timing of the instruction mix is
+the point. Variants (template V): 0 = MFMAs only (barriers kept), 1 = MFMAs + fragment reads,
+2 = full loop with reads and DMA spread through the MFMAs, 3 = full loop with each part's reads and
+DMA issued as one burst before its MFMAs, 4 = V2 followed by a register epilogue (16-B nontemporal
+stores of 256-B row segments, no LDS) into the tile of a [65536][3072] bf16 output.
+  python3 tools/mb/gen_g4loop.py && hipcc -O3 --offload-arch=gfx950 tools/mb/g4loop.hip -o tools/mb/g4loop
+"""
+import os
+
+NR = 16  # fragment reads per part (8 A + 8 B)
+ND = 8   # DMA pieces per part
+
+
+def mfma(i, j, kc):
+    a0 = 4 * (8 * i + j)
+    av = (68 if kc == 0 else 100) + 4 * i
+    bv = (4 if kc == 0 else 36) + 4 * j
+    return f"v_mfma_f32_16x16x32_bf16 a[{a0}:{a0 + 3}], v[{av}:{av + 3}], v[{bv}:{bv + 3}], a[{a0}:{a0 + 3}]"
+
+
+def reads(kc_dst, stage_addr_a, stage_addr_b, kc_src):
+    """16 ds_read_b128: A fragments i (8) then B fragments j (8) of K half kc_src into the kc_dst set"""
+    out = []
+    for i in range(8):
+        d = (68 if kc_dst == 0 else 100) + 4 * i
+        out.append(f"ds_read_b128 v[{d}:{d + 3}], {stage_addr_a} offset:{kc_src * 16384 + i * 1024}")
+    for j in range(8):
+        d = (4 if kc_dst == 0 else 36) + 4 * j
+        out.append(f"ds_read_b128 v[{d}:{d + 3}], {stage_addr_b} offset:{kc_src * 16384 + j * 1024}")
+    return out
+
+
+def dmas(part):
+    """8 LDS-DMA pieces: 4 into the wave's quarter of the A region, 4 into its quarter of the B
+    region of K half `part` (kc0 in part A, kc1 in part B) of the current stage. m0 walks s42 (A) /
+    s43 (B). The sources are the real operand rows: piece p of a wave covers 16 rows x 64 B (one K
+    half) of A[m0 + 64 wave + 16 p ..][k] / B[n0 + ...][k] (K-contiguous, K * 2 bytes per row): source
+    offset s40 (= 128 B x the iteration's K-tile) + 64 x half + p x %[pstep] (16 rows)."""
+    out = []
+    for p in range(ND):
+        reg, vo, rs = ("s42", "%[voffa]", "%[srda]") if p < 4 else ("s43", "%[voffb]", "%[srdb]")
+        step = [f"s_add_u32 s41, s40, {part * 64}"] if p % 4 == 0 else ["s_add_u32 s41, s41, %[pstep]"]
+        out.append([f"s_mov_b32 m0, {reg}"] + step +
+                   [f"buffer_load_dwordx4 {vo}, {rs}, s41 offen lds", f"s_add_u32 {reg}, {reg}, 1024"])
+    return out
+
+
+def part(kc, v, rd, dm):
+    """64 MFMAs of K half kc with the reads rd and DMA pieces dm placed per variant v"""
+    mf = [mfma(i, j, kc) for i in range(8) for j in range(8)]
+    lines = []
+    if v == 3:  # bursts first
+        lines += rd
+        for d in dm:
+            lines += d
+        lines += mf
+        return lines
+    ri = di = 0
+    for k, m in enumerate(mf):
+        lines.append(m)
+        if v >= 1 and k % 4 == 0 and ri < len(rd):
+            lines.append(rd[ri]); ri += 1
+        if v in (2, 4) and k % 8 == 2 and di < len(dm):
+            lines += dm[di]; di += 1
+    assert ri == len(rd) and di == len(dm)
+    return lines
+
+
+def kernel(v):
+    L = []
+    # prologue: zero the accumulators, DMA iterations 0 (stage 0) and 1 (stage 1), wait for 0's kc0
+    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    L += ["s_mov_b32 s44, %[nit]", "s_mov_b32 s40, 0", "s_mov_b32 s45, 0"]
+    for st in (0, 1):
+        for half in (0, 1):
+            L += [f"s_add_u32 s42, %[mA], {st * 65536 + half * 16384}", f"s_add_u32 s43, %[mB], {st * 65536 + half * 16384}"]
+            if v >= 2:
+                for d in dmas(half):
+                    L += d
+        L += ["s_add_u32 s40, s40, 128"]
+    if v >= 2:
+        L += ["s_waitcnt vmcnt(24)"]
+    L += ["s_barrier"]
+    if v >= 1:
+        L += reads(0, "%[rA0]", "%[rB0]", 0)
+    # the loop: s45 = 0 / 1 = t % 2; s40 = source offset of iteration t + 2
+    L += ["L_top_%=:"]
+    L += ["s_waitcnt vmcnt(16) lgkmcnt(0)" if v >= 2 else "s_waitcnt lgkmcnt(0)", "s_barrier"]
+    L += ["s_cmp_eq_u32 s45, 0"]
+    L += ["s_cselect_b32 s42, %[mA], %[mA1]", "s_cselect_b32 s43, %[mB], %[mB1]"]
+    # part A: kc1 reads of stage t%2 (address registers chosen by branch-free selects would need a
+    # VGPR select; the two stages are two code paths instead)
+    body = {}
+    for st in (0, 1):
+        rA, rB = ("%[rA0]", "%[rB0]") if st == 0 else ("%[rA1]", "%[rB1]")
+        nA, nB = ("%[rA1]", "%[rB1]") if st == 0 else ("%[rA0]", "%[rB0]")
+        rdA = reads(1, rA, rB, 1) if v >= 1 else []
+        dmA = dmas(0) if v >= 2 else []
+        pa = part(0, v, rdA, dmA)
+        mid = ["s_waitcnt vmcnt(16) lgkmcnt(0)" if v >= 2 else "s_waitcnt lgkmcnt(0)", "s_barrier"]
+        mid += [f"s_add_u32 s42, %[mA{'' if st == 0 else '1'}], 16384", f"s_add_u32 s43, %[mB{'' if st == 0 else '1'}], 16384"]
+        rdB = reads(0, nA, nB, 0) if v >= 1 else []
+        dmB = dmas(1) if v >= 2 else []
+        pb = part(1, v, rdB, dmB)
+        body[st] = pa + mid + pb
+    L += ["s_cbranch_scc0 L_odd_%="]
+    L += body[0]
+    L += ["s_branch L_next_%="]
+    L += ["L_odd_%=:"]
+    L += body[1]
+    L += ["L_next_%=:"]
+    L += ["s_xor_b32 s45, s45, 1", "s_add_u32 s40, s40, 128",
+          "s_sub_u32 s44, s44, 1", "s_cmp_eq_u32 s44, 0", "s_cbranch_scc0 L_top_%="]
+    L += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    if v == 4:  # register epilogue: 8 accumulators of a row -> 8 consecutive bf16 columns, 16-B stores
+        L += ["s_mov_b32 s41, 0"]
+        for i in range(8):
+            for e in range(4):
+                L += [f"v_accvgpr_read_b32 v{4 + j}, a{4 * (8 * i + j) + e}" for j in range(8)]
+                L += [f"v_cvt_pk_bf16_f32 v{12 + q}, v{4 + 2 * q}, v{5 + 2 * q}" for q in range(4)]
+                L += ["buffer_store_dwordx4 v[12:15], %[voffc], %[srdc], s41 offen nt"]
+                L += ["s_add_u32 s41, s41, %[ldc2]"]
+            L += ["s_add_u32 s41, s41, %[ldc2x12]"]
+    return L
+
+
+def emit():
+    clob = [f'"v{r}"' for r in range(4, 132)] + [f'"a{r}"' for r in range(256)] + \
+           [f'"s{r}"' for r in range(40, 47)] + ['"m0"', '"scc"', '"memory"']
+    parts = []
+    for v in range(5):
+        asm = "\\n\\t".join(kernel(v))
+        parts.append(f"""
+template <> __device__ __forceinline__ void loop<{v}>(const LoopArgs& x) {{
+  asm volatile("{asm}"
+      :
+      : [voffa] "v"(x.voffa), [voffb] "v"(x.voffb), [srda] "s"(x.srda), [srdb] "s"(x.srdb), [nit] "s"(x.nit),
+        [pstep] "s"(x.pstep), [mA] "s"(x.mA), [mB] "s"(x.mB), [mA1] "s"(x.mA1), [mB1] "s"(x.mB1),
+        [rA0] "v"(x.rA0), [rB0] "v"(x.rB0), [rA1] "v"(x.rA1), [rB1] "v"(x.rB1),
+        [voffc] "v"(x.voffc), [srdc] "s"(x.srdc), [ldc2] "s"(x.ldc2), [ldc2x12] "s"(x.ldc2x12)
+      : {", ".join(clob)});
+}}""")
+    src = HEADER + "".join(parts) + FOOTER
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "g4loop.hip"), "w") as f:
+        f.write(src)
+
+
+HEADER = r'''// GENERATED by tools/mb/gen_g4loop.py — the four-wave bf16 GEMM main loop as one inline-assembly
+// block (see the generator's docstring). Timing only: no result is checked.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+struct LoopArgs {
+  uint32_t voffa, voffb;               // per lane: source byte offset of its 16 B (row wave*64 + lane/4, chunk lane%4)
+  __amdgpu_buffer_rsrc_t srda, srdb;   // the tile's A rows [m0, m0+256) and B rows [n0, n0+256), K-contiguous
+  uint32_t nit, pstep;                 // K-tiles; 16 rows of an operand in bytes
+  uint32_t mA, mB, mA1, mB1;           // LDS DMA destinations (wave quarter of the A / B regions), stage 0 / 1
+  uint32_t rA0, rB0, rA1, rB1;         // per lane: fragment read addresses (A / B, stage 0 / 1)
+  uint32_t voffc;                      // V4 epilogue: per lane byte offset of its first 16-B output chunk
+  __amdgpu_buffer_rsrc_t srdc;         // V4 epilogue: the workgroup's output tile
+  uint32_t ldc2, ldc2x12;              // output row pitch in bytes, and 12 rows of it
+};
+template <int V> __device__ void loop(const LoopArgs& x);
+'''
+
+FOOTER = r'''
+
+// tile order: XG = 0: row-major over (M-tile, N-tile); XG = 1: each XCD (blockIdx % 8) walks a
+// contiguous run of the row-major tiles, so the tiles sharing an A panel run on one XCD's L2
+template <int V>
+__global__ void __launch_bounds__(256) g4loop_kernel(const __bf16* A, const __bf16* B, int K, int ntn, int xg,
+                                                     uint64_t* ticks, void* out) {
+  __shared__ __attribute__((aligned(1024))) char smem[131072];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t base = (uint32_t)(size_t)smem;
+  const uint32_t nb = gridDim.x, b0 = blockIdx.x;
+  const uint32_t bid = xg ? (b0 % 8u) * (nb / 8u) + b0 / 8u : b0;
+  const uint32_t tm = bid / (uint32_t)ntn, tn = bid % (uint32_t)ntn;
+  LoopArgs x;
+  const uint32_t rowb = (uint32_t)K * 2u;
+  x.voffa = (uint32_t)(wave * 64 + (lane >> 2)) * rowb + (uint32_t)(lane & 3) * 16u;
+  x.voffb = x.voffa;
+  x.srda = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A) + (size_t)tm * 256u * K, 0, (int)(256u * rowb), 0x00020000);
+  x.srdb = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(B) + (size_t)tn * 256u * K, 0, (int)(256u * rowb), 0x00020000);
+  x.nit = (uint32_t)(K / 64);
+  x.pstep = 16u * rowb;
+  // stage s: A-kc0 at +0, A-kc1 +16K, B-kc0 +32K, B-kc1 +48K; a wave fills its 4-KB quarter of each
+  x.mA = base + wave * 4096; x.mB = base + 32768 + wave * 4096;
+  x.mA1 = x.mA + 65536; x.mB1 = x.mB + 65536;
+  // fragment i of a wave's 128 rows: 1 KB at (wave / 2) * 8 KB + i KB of the A region, lane-linear
+  x.rA0 = base + (wave >> 1) * 8192 + lane * 16;
+  x.rB0 = base + 32768 + (wave & 1) * 8192 + lane * 16;
+  x.rA1 = x.rA0 + 65536; x.rB1 = x.rB0 + 65536;
+  // V4 output: the tile of a [M][ntn * 256] bf16 matrix; wave (wm, wn) owns rows wm*128 + 16 i +
+  // 4 (lane / 16) + e and columns wn*128 + 8 (lane % 16) + j (B fragment j holds the columns 8 c + j,
+  // so a lane's 8 accumulators of a row are 8 consecutive columns)
+  const uint32_t ldc = (uint32_t)ntn * 256u;
+  x.ldc2 = ldc * 2u; x.ldc2x12 = 12u * ldc * 2u;
+  const size_t tile0 = ((size_t)tm * 256u * ldc + (size_t)tn * 256u) * 2u;
+  x.srdc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + tile0, 0, 0x7fffffff, 0x00020000);
+  x.voffc = (((wave >> 1) * 128u + 4u * (lane >> 4)) * ldc + (wave & 1) * 128u + 8u * (lane & 15)) * 2u;
+  __syncthreads();
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  loop<V>(x);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0 && blockIdx.x < 4096) ticks[blockIdx.x * 4 + wave] = t1 - t0;
+}
+
+template <int V>
+static void run(const char* name, const char* shape, const __bf16* A, const __bf16* B, int M, int N, int K, int xg,
+                uint64_t* ticks, void* out) {
+  const int grid = (M / 256) * (N / 256), ntn = N / 256;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(g4loop_kernel<V>, dim3(grid), dim3(256), 0, 0, A, B, K, ntn, xg, ticks, out);
+  const int reps = 10;
+  hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(g4loop_kernel<V>, dim3(grid), dim3(256), 0, 0, A, B, K, ntn, xg, ticks, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  const int n = grid < 4096 ? grid : 4096;
+  uint64_t* h = (uint64_t*)malloc(n * 4 * 8);
+  hipMemcpy(h, ticks, n * 4 * 8, hipMemcpyDeviceToHost);
+  double m = 0;
+  for (int i = 0; i < n * 4; ++i) m += (double)h[i];
+  m /= n * 4;
+  free(h);
+  const double us = 1e3 * ms / reps;
+  const double tf = 2.0 * M * N * (double)K / (us * 1e-6) / 1e12;
+  printf("%-8s M %6d N %5d K %5d xg %d  %-32s %8.1f us %7.1f TFLOP/s %6.0f cycles/K-tile (per wave, incl. prologue%s)\n",
+         shape, M, N, K, xg, name, us, tf, m / (K / 64), V == 4 ? " + epilogue" : "");
+  hipEventDestroy(e0); hipEventDestroy(e1);
+}
+
+int main() {
+  // the bf16 encoder forward shapes of profiles/r05_bf16_gemm_vs_hipblaslt.log (M = tokens)
+  struct S { const char* name; int M, N, K; } shapes[] = {
+      {"qkv", 65536, 2304, 768}, {"out", 65536, 768, 768}, {"ffn1", 65536, 3072, 768}, {"ffn2", 65536, 768, 3072},
+      {"vit-ffn1", 100864 / 256 * 256, 3072, 768}};
+  size_t abytes = (size_t)100864 * 3072 * 2, bbytes = (size_t)3072 * 3072 * 2;
+  __bf16 *A, *B;
+  hipMalloc(&A, abytes); hipMalloc(&B, bbytes);
+  hipMemset(A, 0, abytes); hipMemset(B, 0, bbytes);
+  uint64_t* ticks;
+  hipMalloc(&ticks, 4096 * 4 * 8);
+  void* out;
+  hipMalloc(&out, (size_t)100864 * 3072 * 2);
+  for (const S& s : shapes)
+    for (int xg = 0; xg < 2; ++xg) {
+      run<0>("V0 MFMA only", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<1>("V1 MFMA + fragment reads", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<2>("V2 MFMA + reads + DMA, spread", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<3>("V3 MFMA + reads + DMA, bursts", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<4>("V4 = V2 + register epilogue", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+    }
+  hipError_t err = hipDeviceSynchronize();
+  printf("status: %s\n", hipGetErrorString(err));
+  return err == hipSuccess ? 0 : 1;
+}
+'''
+
+if __name__ == "__main__":
+    emit()
