@@ -457,7 +457,7 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
         return None
     M, K = A.shape
     N = B.shape[0]
-    if M % 256 or N % 256 or K % 64 or K < 64 or K > 1024:
+    if M % 256 or N % 256 or K % 64 or K < 64 or K > int(os.environ.get("MMFD_G4_KMAX", "1024")):
         return None
     ts = [t for t in (A, B, out, residual, aux, bias) if t is not None]
     if any(t.data_ptr() % 16 for t in ts) or any(_ld(t) % 8 for t in (A, B, out, residual, aux) if t is not None):
@@ -466,7 +466,7 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
         return 0
     if act == ACT_NONE and residual is not None and not residual_first:
         return 2 if dropout_p > 0 else 1
-    if act == ACT_GELU and residual is None and dropout_p <= 0:
+    if act == ACT_GELU and residual is None and dropout_p <= 0 and os.environ.get("MMFD_G4_GELU"):
         return 3
     return None
 

@@ -118,6 +118,7 @@ def test_gemm_bf16_g4_epilogues_match_g8(mode, monkeypatch):
     bias = _rand(N, seed=53).to(DEV)
     res = _rand(M, N, dtype=torch.bfloat16, seed=54).to(DEV)
     outs = {}
+    monkeypatch.setenv("MMFD_G4_GELU", "1")  # (the GELU mode is opt-in in the step, see gemm_g4.hip)
     for g4 in ("1", "0"):
         monkeypatch.setenv("MMFD_G4", g4)
         aux = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)

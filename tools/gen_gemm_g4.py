@@ -26,8 +26,8 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "mb"))
 import gen_g4loop as G  # noqa: E402  (mfma / reads / part: the measured schedule)
 
-OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                   "multimodal-misinformation-detection_amd", "csrc", "gemm_g4.hip")
+OUT = os.environ.get("G4_OUT") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "multimodal-misinformation-detection_amd", "csrc", "gemm_g4.hip")
 
 
 def dmas(part):
@@ -250,13 +250,17 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   // K <= 1024: the short-K products (QKV, attention output, FFN1 at K = 768) gain from the register
   // epilogue; at K = 3072 (FFN2) the power-limited main loop is no faster than gemm256_kernel's and
   // ViT's FFN2 measured 10 % slower (profiles/r05_g4_vs_g8_vs_hipblaslt.log)
-  if (a.K > 1024) return false;
+  static const int64_t kmax = getenv("MMFD_G4_KMAX") ? atoll(getenv("MMFD_G4_KMAX")) : 1024;  // A/B override
+  if (a.K > kmax) return false;
   if (!e.vec || e.pl || e.beta != 0.0f) return false;
   // the epilogue modes of the encoder forward Linears (anything else runs on gemm256_kernel)
   int epi = -1;
   if (e.act == MMFD_ACT_NONE && !e.residual && e.p <= 0.0f) epi = 0;                    // QKV
   else if (e.act == MMFD_ACT_NONE && e.residual && !e.res_first) epi = e.p > 0.0f ? 2 : 1;  // out / FFN2
-  else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f) epi = 3;                // FFN1
+  // FFN1 (bias + GELU + pre-activation): measured 0.89-1.03x of gemm256_kernel across boxes (its
+  // time is the GELU's VALU work, which one wave per SIMD does not hide better than two;
+  // profiles/r05_g4_schedule_ab.log): left on gemm256_kernel unless MMFD_G4_GELU=1
+  else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f && getenv("MMFD_G4_GELU")) epi = 3;
   if (epi < 0) return false;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al16(a.A) || !al16(a.B) || !al16(a.C)) return false;

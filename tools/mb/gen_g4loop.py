@@ -72,11 +72,12 @@ def part(kc, v, rd, dm):
         lines += mf
         return lines
     ri = di = 0
+    ra, da = int(os.environ.get("G4_READ_AT", "0")), int(os.environ.get("G4_DMA_AT", "2"))  # schedule A/B
     for k, m in enumerate(mf):
         lines.append(m)
-        if v >= 1 and k % 4 == 0 and ri < len(rd):
+        if v >= 1 and k % 4 == ra and ri < len(rd):
             lines.append(rd[ri]); ri += 1
-        if v in (2, 4) and k % 8 == 2 and di < len(dm):
+        if v in (2, 4) and k % 8 == da and di < len(dm):
             lines += dm[di]; di += 1
     assert ri == len(rd) and di == len(dm)
     return lines
