@@ -47,7 +47,8 @@ def dmas(part):
 
 
 def body():
-    L = [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    # m0 is reserved to the compiler: saved here and restored at the end (the DMA pieces walk it)
+    L = ["s_mov_b32 s47, m0"] + [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
     L += ["s_mov_b32 s44, %[nit]", "s_mov_b32 s40, 0", "s_mov_b32 s45, 0"]
     for st in (0, 1):  # prologue: K-tiles 0 and 1 into stages 0 and 1
         for half in (0, 1):
@@ -73,7 +74,7 @@ def body():
           "s_cbranch_scc0 L_top_%="]
     # the pieces fetched past the last K-tile land in stages nobody reads; drain them before the
     # workgroup's LDS can be reused
-    L += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    L += ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_mov_b32 m0, s47"]
     return L
 
 
@@ -285,7 +286,7 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
 
 def main():
     clob = [f'"v{r}"' for r in range(4, 132)] + [f'"a{r}"' for r in range(256)] + \
-           [f'"s{r}"' for r in range(40, 47)] + ['"m0"', '"scc"', '"memory"']
+           [f'"s{r}"' for r in range(40, 48)] + ['"scc"', '"memory"']
     src = SRC.replace("@ASM@", "\\n\\t".join(body())).replace("@CLOB@", ", ".join(clob)).replace("@ACCREADS@", acc_reads())
     with open(OUT, "w") as f:
         f.write(src)
