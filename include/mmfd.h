@@ -48,7 +48,7 @@ const char* mmfd_last_error_string(void);
 /* ABI version of this header: bumped on every change of an argument struct's layout (2: struct_size
    at the head of mmfd_gemm_args / mmfd_attn_args, mmfd_attn_args.drop_mask). mmfd_version() returns
    the library's; a caller compares it with MMFD_ABI_VERSION before its first call. */
-#define MMFD_ABI_VERSION 2
+#define MMFD_ABI_VERSION 3
 int mmfd_version(void);
 /* 32-bit dropout hash (host copy of the device function), for tests and the CPU oracle. */
 uint32_t mmfd_dropout_hash(uint64_t seed, uint64_t salt, uint64_t index);
@@ -132,6 +132,15 @@ int mmfd_set_fp32_gemm_mode(int mode);
    plane pair; env MMFD_X6_SEGMENTED). The host-side planning of which tensors may exist only as
    planes (mmfd.kernels.x6_ok) asks this, so it honours every switch the library does. */
 int mmfd_gemm_runs_split(const mmfd_gemm_args* args);
+/* the four-wave assembly-scheduled bf16 forward GEMM (gemm_g4.hip): mode 0 = off (those products run
+   on the 256x256 eight-wave kernel), 1 = on for the bias / residual / dropout + residual epilogues
+   (default), 2 = also the GELU + pre-activation epilogue; -1 only queries. Load-time defaults from
+   env MMFD_G4=0 / MMFD_G4_GELU=1. Returns the previous mode (A/B measurements and tests; not per
+   stream: set it between launches). */
+int mmfd_set_g4_mode(int mode);
+/* the largest K the four-wave GEMM takes (default 1024, env MMFD_G4_KMAX); kmax <= 0 only queries.
+   Returns the previous limit. */
+int64_t mmfd_set_g4_kmax(int64_t kmax);
 /* fp32 [rows][ld] -> bf16 planes [3][rows][cols] (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid);
    cols % 8 == 0, 16-B aligned rows) */
 int mmfd_split3(int64_t rows, int64_t cols, const float* x, int64_t ld, void* planes, mmfd_stream_t stream);
@@ -309,10 +318,12 @@ int mmfd_attn_fill_masked_rows(int dtype, int64_t B, int64_t H, int64_t L, int64
 /* scatter-add the gradient of the pre-LN sum into the three tables (modeling_bert.py BertEmbeddings:
    word[id] += row, pos[t] += row, type[tt] += row), deterministically: the word rows are stably
    radix-sorted by id and each id's rows summed in row order by one writer; the type table reduces
-   fixed row slabs in order. workspace >= mmfd_embed_bwd_workspace_bytes(B, L, D); ids < 2^32,
-   B*L < 2^31. dword / dpos / dtype_emb may each be NULL (that table is skipped). */
+   fixed row slabs in order. vocab = rows of the word table (ids in [0, vocab)): the sort runs over
+   the ceil(log2(vocab)) id bits only (<= 0: all 32 bits; ABI 3 added it). workspace >=
+   mmfd_embed_bwd_workspace_bytes(B, L, D); ids < 2^32, B*L < 2^31. dword / dpos / dtype_emb may each
+   be NULL (that table is skipped). */
 int64_t mmfd_embed_bwd_workspace_bytes(int64_t B, int64_t L, int64_t D);
-int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, int64_t vocab, const int64_t* input_ids,
                    const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos,
                    float* dtype_emb, int64_t padding_idx, void* workspace, int64_t workspace_bytes,
                    mmfd_stream_t stream);

@@ -1468,6 +1468,9 @@ int g_v2_generic = [] {
   return v && atoi(v) != 0 ? 1 : 0;
 }();
 
+// A/B switch: MMFD_ATTN_V1=1 sends every call to the streaming v1 kernels (read once, not per launch)
+const bool g_attn_v1 = getenv("MMFD_ATTN_V1") != nullptr;
+
 int g_fp32_attn_mode = [] {
   const char* v = getenv("MMFD_FP32_ATTN");
   const char* gm = getenv("MMFD_FP32_GEMM");
@@ -2293,7 +2296,7 @@ bool x6_attn_ok(const mmfd_attn_args& a, bool bwd) {
   if (v2_pad(a.Lk, 16) > X6A_LMAX || (bwd && v2_pad(a.Lq, 16) > X6A_LMAX)) return false;
   // dropout indices advanced in 32 bits (hash_c1)
   if (a.dropout_p > 0.f && (uint64_t)a.B * (uint64_t)a.H * (uint64_t)a.Lq * (uint64_t)a.Lk > (1ull << 32)) return false;
-  return !getenv("MMFD_ATTN_V1");
+  return !g_attn_v1;
 }
 
 template <int D, bool DROP>
@@ -2533,7 +2536,7 @@ extern "C" int mmfd_attn_fwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   // (fp32 K/V images of 512 keys would not fit the LDS)
   const bool bf = a->dtype == MMFD_BF16;
   const bool x6 = x6_attn_ok(*a, false);
-  const bool v2 = x6 || ((p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !getenv("MMFD_ATTN_V1"));
+  const bool v2 = x6 || ((p.Lk <= V2_LMAX || (bf && p.Lk <= V2_LMAX_FWD && p.B * p.H >= 256)) && !g_attn_v1);
   MMFD_CHECK_ARG(!a->cos_logit_scale || (v2 && bf && a->rel_bias),
                  "attn_fwd: cosine attention needs bf16, the resident-K/V kernel (Lk <= 256) and a rel_bias");
   p.pl = nullptr; p.pl_only = 0;
@@ -2567,7 +2570,7 @@ extern "C" int mmfd_attn_bwd(const mmfd_attn_args* a, mmfd_stream_t stream) {
   if (p.B == 0 || p.Lq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const bool x6 = x6_attn_ok(*a, true);
-  const bool v2 = x6 || (p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !getenv("MMFD_ATTN_V1"));
+  const bool v2 = x6 || (p.Lk <= V2_LMAX && p.Lq <= V2_LMAX && !g_attn_v1);
   p.pl = nullptr; p.pl_only = 0;
   const int64_t W = 3 * a->H * a->D;
   if (a->dqkv_planes) {

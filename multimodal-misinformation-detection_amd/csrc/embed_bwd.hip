@@ -3,7 +3,8 @@
 //
 // The word table is a scatter-add over repeated token ids. Since round 5 it is no longer done with
 // fp32 atomics (whose order, and so the last bits of the result, changed from run to run): the
-// token rows are stably radix-sorted by id (hipCUB), each id's rows are summed in row order in
+// token rows are stably radix-sorted by id (rocPRIM, over the id bits of the vocabulary only:
+// 15 for BERT's 30,522 rows, two 8-bit digit passes instead of four), each id's rows are summed in row order in
 // pieces of at most kSegChunk sorted rows, and the pieces are added in order by a single writer
 // per table row. The
 // token-type table (two rows) sums fixed row slabs into workspace partials and reduces the slabs in
@@ -11,7 +12,7 @@
 // which the graph-captured data-parallel step's self-check (mmfd.dp, tests/test_dp_gpu.py) relies on.
 #include "common.h"
 #include <algorithm>
-#include <hipcub/device/device_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 namespace {
 constexpr int kTypeSlabs = 1024;
@@ -177,9 +178,10 @@ struct EmbedWs {
 };
 hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
   size_t tmp = 0;
-  hipcub::DoubleBuffer<uint32_t> k(nullptr, nullptr);
-  hipcub::DoubleBuffer<int32_t> v(nullptr, nullptr);
-  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, v, (int)rows, 0, 32, (hipStream_t)0);
+  rocprim::double_buffer<uint32_t> k(nullptr, nullptr);
+  rocprim::double_buffer<int32_t> v(nullptr, nullptr);
+  // the temporary storage of the widest sort (all 32 key bits): an upper bound for every end_bit
+  const hipError_t e = rocprim::radix_sort_pairs(nullptr, tmp, k, v, (size_t)rows, 0, 32, (hipStream_t)0);
   int64_t o = 0;
   w.keys0 = o; o += align256(rows * 4);
   w.keys1 = o; o += align256(rows * 4);
@@ -193,6 +195,13 @@ hipError_t embed_ws_layout(int64_t rows, int64_t D, EmbedWs& w) {
   w.total = o;
   return e;
 }
+// key bits that hold every id < vocab (all 32 when the vocabulary is not given)
+unsigned id_bits(int64_t vocab) {
+  if (vocab <= 0 || vocab > ((int64_t)1 << 32)) return 32;
+  unsigned b = 1;
+  while (b < 32 && ((int64_t)1 << b) < vocab) ++b;
+  return b;
+}
 int type_slabs(int64_t rows) { return (int)std::min<int64_t>(kTypeSlabs, std::max<int64_t>(1, rows / 64)); }
 }  // namespace
 
@@ -203,7 +212,7 @@ extern "C" int64_t mmfd_embed_bwd_workspace_bytes(int64_t B, int64_t L, int64_t 
   return w.total;
 }
 
-extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const int64_t* input_ids,
+extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, int64_t vocab, const int64_t* input_ids,
                               const int64_t* token_type_ids, const void* dsum, float* dword, float* dpos, float* dtype_emb,
                               int64_t padding_idx, void* workspace, int64_t workspace_bytes, mmfd_stream_t stream) {
   const int64_t rows = B * L;
@@ -220,23 +229,23 @@ extern "C" int mmfd_embed_bwd(int dtype, int64_t B, int64_t L, int64_t D, const 
   char* ws = (char*)workspace;
   const bool bf = dtype == MMFD_BF16;
   if (dword) {
-    hipcub::DoubleBuffer<uint32_t> k((uint32_t*)(ws + w.keys0), (uint32_t*)(ws + w.keys1));
-    hipcub::DoubleBuffer<int32_t> v((int32_t*)(ws + w.vals0), (int32_t*)(ws + w.vals1));
-    hipLaunchKernelGGL(embed_sort_prep_kernel, dim3(gridn(rows, 256)), dim3(256), 0, s, rows, input_ids, k.Current(),
-                       v.Current());
+    rocprim::double_buffer<uint32_t> k((uint32_t*)(ws + w.keys0), (uint32_t*)(ws + w.keys1));
+    rocprim::double_buffer<int32_t> v((int32_t*)(ws + w.vals0), (int32_t*)(ws + w.vals1));
+    hipLaunchKernelGGL(embed_sort_prep_kernel, dim3(gridn(rows, 256)), dim3(256), 0, s, rows, input_ids, k.current(),
+                       v.current());
     size_t tmp = (size_t)w.sort_tmp_bytes;
-    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort_tmp, tmp, k, v, (int)rows, 0, 32, s);
+    const hipError_t e = rocprim::radix_sort_pairs(ws + w.sort_tmp, tmp, k, v, (size_t)rows, 0, id_bits(vocab), s);
     if (e != hipSuccess) return mmfd_set_error((int)e, "embed_bwd: radix sort: %s", hipGetErrorString(e));
     const dim3 g((unsigned)((rows + kSegChunk - 1) / kSegChunk));
     float* pf = (float*)(ws + w.seg_first);
     float* pl = (float*)(ws + w.seg_last);
     if (bf)
-      hipLaunchKernelGGL((embed_word_segsum_kernel<bf16>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
+      hipLaunchKernelGGL((embed_word_segsum_kernel<bf16>), g, dim3(256), 0, s, rows, D, k.current(), v.current(),
                          (const bf16*)dsum, dword, pf, pl, padding_idx);
     else
-      hipLaunchKernelGGL((embed_word_segsum_kernel<float>), g, dim3(256), 0, s, rows, D, k.Current(), v.Current(),
+      hipLaunchKernelGGL((embed_word_segsum_kernel<float>), g, dim3(256), 0, s, rows, D, k.current(), v.current(),
                          (const float*)dsum, dword, pf, pl, padding_idx);
-    hipLaunchKernelGGL(embed_word_join_kernel, g, dim3(256), 0, s, rows, D, k.Current(), pf, pl, dword, padding_idx);
+    hipLaunchKernelGGL(embed_word_join_kernel, g, dim3(256), 0, s, rows, D, k.current(), pf, pl, dword, padding_idx);
   }
   if (dpos) {
     if (bf) hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16>), dim3(gridn(L * D, 256)), dim3(256), 0, s, B, L, D, (const bf16*)dsum, dpos);

@@ -141,10 +141,16 @@ class GradAllReduce:
         """Make every rank start from rank `src`'s parameters (called once when a trainer is built:
         ranks may have initialised their replicas from different seeds). Parameters are flattened
         into bucket-sized fp32 buffers, one broadcast per bucket; the copies back are plain
-        in-place writes, so bf16 weight shadows built later see the broadcast values."""
+        in-place writes (they bump each parameter's version counter, so the bf16 weight shadows
+        are re-cast from the broadcast values)."""
+        self.broadcast_tensors(params, src)
+
+    def broadcast_tensors(self, tensors, src=0):
+        """rank `src`'s values of `tensors` (fp32, any shapes; None entries skipped) on every rank,
+        in bucket-sized broadcasts on `group`"""
         if not self._active():
             return
-        params = [p for p in params]
+        params = [p for p in tensors if p is not None]
         i = 0
         while i < len(params):
             j, n = i, 0
@@ -174,10 +180,19 @@ class GradAllReduce:
     # ---- graph capture -------------------------------------------------------------------------------
     def capture_group(self):
         """The process group the captured step's all-reduces run on (collective: every rank calls it
-        at the same point; created once). Same ranks as `group`; with a device-bound default group
-        (init_process_group(device_id=...), as bench.py and train.py do) its communicator is
-        connected at creation, so no collective ever runs on it outside a capture."""
+        at the same point; created once — FusionTrainer.capture calls it BEFORE its eager warm-up
+        steps, so a rank that fails later cannot leave the others waiting inside new_group). Same
+        ranks as `group`; with a device-bound default group (init_process_group(device_id=...), as
+        bench.py and train.py do) its communicator is connected at creation, so no collective ever
+        runs on it outside a capture. An RCCL default group WITHOUT a bound device would connect the
+        new communicator lazily — inside the capture — so that case is refused (every rank raises
+        the same error before any collective; capture_dp_step then runs eager steps)."""
         if self._capture_group is None:
+            if dist.get_backend(self.group) == "nccl":
+                from torch.distributed import distributed_c10d as c10d
+                if getattr(c10d._get_default_group(), "bound_device_id", None) is None:
+                    raise RuntimeError("mmfd DP capture needs a device-bound default process group "
+                                       "(init_process_group(..., device_id=torch.device('cuda', local_rank)))")
             ranks = None if self.group is None else dist.get_process_group_ranks(self.group)
             self._capture_group = dist.new_group(ranks=ranks, group_desc="mmfd_dp_capture")
         return self._capture_group

@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MMFD_LIB_PATH") or os.path.join(_HERE, "libmmfd_hip.s
 TORCH_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libmmfd_torch.so")
 
 F32, BF16, F16 = 0, 1, 2
-ABI_VERSION = 2  # include/mmfd.h MMFD_ABI_VERSION: the layout of the argument structs below
+ABI_VERSION = 3  # include/mmfd.h MMFD_ABI_VERSION: the layout of the argument structs below
 COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
 
@@ -131,6 +131,8 @@ SIGNATURES = {
     "mmfd_set_fp32_attn_mode": (_I, [_I]),
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_gemm_runs_split": (_I, [ctypes.POINTER(GemmArgs)]),
+    "mmfd_set_g4_mode": (_I, [_I]),
+    "mmfd_set_g4_kmax": (_I64, [_I64]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
     "mmfd_layernorm_fwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP, _VP]),
     "mmfd_layernorm_bwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP,
@@ -146,7 +148,7 @@ SIGNATURES = {
     "mmfd_xent_fwd_bwd": (_I, [_I, _I64, _I64, _VP, _VP, _VP, _I64, _VP, _I, _VP, _VP, _VP]),
     "mmfd_embed_ln_fwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
                                _F, _VP, _U64, _VP]),
-    "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP]),
+    "mmfd_embed_bwd": (_I, [_I, _I64, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP]),
     "mmfd_embed_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "mmfd_mask_to_bias": (_I, [_I64, _VP, _VP, _F, _VP]),
     "mmfd_embed_ln_fwd_ex": (_I, [_I, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP,
@@ -360,6 +362,24 @@ def set_fp32_attn_mode(mode):
     return {0: "native", 1: "split"}[old]
 
 
+_G4_MODES = {"off": 0, "on": 1, "gelu": 2}
+
+
+def set_g4_mode(mode=None, kmax=None):
+    """The four-wave bf16 forward GEMM (gemm_g4.hip): 'off', 'on' (default) or 'gelu' (the FFN1 GELU
+    epilogue too), and the largest K it takes. Returns the previous (mode, kmax); None leaves a
+    setting as it is (A/B measurements and tests: set between launches, not per stream)."""
+    old = lib().mmfd_set_g4_mode(-1 if mode is None else _G4_MODES[mode])
+    _check(0 if old >= 0 else old, "mmfd_set_g4_mode")
+    old_k = lib().mmfd_set_g4_kmax(0 if kmax is None else int(kmax))
+    return {v: k for k, v in _G4_MODES.items()}[old], int(old_k)
+
+
+def g4_mode():
+    """(mode, kmax) the library currently uses for the four-wave GEMM"""
+    return set_g4_mode()
+
+
 def fp32_gemm_mode():
     global _FP32_MODE
     if _FP32_MODE is None:  # the library's load-time default (env MMFD_FP32_GEMM)
@@ -451,13 +471,14 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
              aux, bias):
     """the four-wave kernel's epilogue mode for this product, or None (mirrors mmfd_gemmx::launch_g4;
     GemmProbe bookkeeping only)"""
-    if os.environ.get("MMFD_G4", "1").startswith("0") or trans_a or trans_b or splits > 1 or a_rowsum is not None:
+    g4, kmax = g4_mode()  # the library's own switches (mmfd_set_g4_mode)
+    if g4 == "off" or trans_a or trans_b or splits > 1 or a_rowsum is not None:
         return None
     if A.dtype != torch.bfloat16 or out.dtype != torch.bfloat16 or alpha != 1.0 or beta != 0.0:
         return None
     M, K = A.shape
     N = B.shape[0]
-    if M % 256 or N % 256 or K % 64 or K < 64 or K > int(os.environ.get("MMFD_G4_KMAX", "1024")):
+    if M % 256 or N % 256 or K % 64 or K < 64 or K > kmax:
         return None
     ts = [t for t in (A, B, out, residual, aux, bias) if t is not None]
     if any(t.data_ptr() % 16 for t in ts) or any(_ld(t) % 8 for t in (A, B, out, residual, aux) if t is not None):
@@ -466,7 +487,7 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
         return 0
     if act == ACT_NONE and residual is not None and not residual_first:
         return 2 if dropout_p > 0 else 1
-    if act == ACT_GELU and residual is None and dropout_p <= 0 and os.environ.get("MMFD_G4_GELU"):
+    if act == ACT_GELU and residual is None and dropout_p <= 0 and g4 == "gelu":
         return 3
     return None
 
@@ -902,7 +923,8 @@ def embed_bwd(ids, tts, dsum, dword, dpos, dtype_emb, padding_idx=-1):
     if nws < 0:
         raise RuntimeError("mmfd_embed_bwd_workspace_bytes failed")
     ws = torch.empty(max(nws, 1), device=dsum.device, dtype=torch.uint8)
-    _check(lib().mmfd_embed_bwd(dtype_code(dsum.dtype), B, L, D, _ptr(ids), _ptr(tts) if tts is not None else None,
+    vocab = dword.shape[0] if dword is not None else 0  # the sort covers the id bits of the vocabulary only
+    _check(lib().mmfd_embed_bwd(dtype_code(dsum.dtype), B, L, D, vocab, _ptr(ids), _ptr(tts) if tts is not None else None,
                                 _ptr(dsum), _ptr(dword), _ptr(dpos), _ptr(dtype_emb), int(padding_idx), _ptr(ws), nws,
                                 _stream()),
            "mmfd_embed_bwd")

@@ -231,6 +231,8 @@ class FusionTrainer:
         `first_loss` keeps the loss vector of the first warm-up step (the first optimizer step of
         this trainer when it is fresh)."""
         self._static = batch
+        if self.dp is not None and self.dp._active():
+            self.dp.capture_group()  # collective: created before the warm-up steps (mmfd.dp)
         s = torch.cuda.Stream(device=self._device())
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -271,6 +273,23 @@ class FusionTrainer:
         """the tensors every rank must agree on after a data-parallel step: the trained parameters'
         gradients, then all parameters"""
         return [p.grad for p in self.params] + [p for p in self.params]
+
+    def resync_state(self, src=0):
+        """Every rank takes rank `src`'s parameters and AdamW state (moments and step counters): the
+        recovery after a captured DP step that failed verify_capture — its verifying replay already
+        ran AdamW on gradients that were not averaged across the ranks, so the replicas (and their
+        moments) diverged, and eager DP steps average gradients but never re-sync parameters. The
+        in-place parameter copies bump the version counters, so the bf16 weight shadows are re-cast."""
+        if self.dp is None or not self.dp._active():
+            return
+        torch.cuda.synchronize()
+        state = []
+        for p in self.params:
+            st = self.optimizer.state.get(p) if self.optimizer is not None else None
+            if st:
+                state += [st.get("exp_avg"), st.get("exp_avg_sq"), st.get("step")]
+        self.dp.broadcast_tensors(list(self.params) + state, src=src)
+        torch.cuda.synchronize()
 
     def release_graph(self):
         """drop the captured step and its private memory pool (eager steps afterwards)"""
@@ -324,9 +343,11 @@ def capture_dp_step(tr, batch, warmup, device, log=logger.info):
         tr.release_graph()
         return False, "capture failed on a rank: eager steps"
     if not tr.verify_capture():
-        log("captured DP step failed the cross-rank checksum; eager steps on every rank")
+        log("captured DP step failed the cross-rank checksum; rank 0's parameters and AdamW state "
+            "re-broadcast, eager steps on every rank")
         tr.release_graph()
-        return False, "captured all-reduce MISMATCH: eager steps"
+        tr.resync_state(src=0)  # the verifying replay stepped AdamW on un-averaged gradients
+        return False, "captured all-reduce MISMATCH: state re-synced from rank 0, eager steps"
     return True, "captured all-reduce verified"
 
 

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in K.SIGNATURES, f"{s} declared in include/mmfd.h but not bound in kernels.py"
-    assert lib.mmfd_version() == K.ABI_VERSION == 2
+    assert lib.mmfd_version() == K.ABI_VERSION == 3
 
 
 def test_host_hash_matches_oracle():
@@ -58,7 +58,7 @@ def test_struct_of_another_abi_layout_is_refused():
     a.dtype = K.BF16
     assert lib.mmfd_gemm(a, None) == 1000  # MMFD_ERR_INVALID
     msg = lib.mmfd_last_error_string().decode()
-    assert "struct_size" in msg and "ABI version 2" in msg, msg
+    assert "struct_size" in msg and f"ABI version {K.ABI_VERSION}" in msg, msg
     assert lib.mmfd_gemm_workspace_bytes(a) == -1 and lib.mmfd_gemm_splits(a) == -1 and lib.mmfd_gemm_runs_split(a) == -1
     for fn in (lib.mmfd_attn_fwd, lib.mmfd_attn_bwd):
         t = K.AttnArgs()

@@ -179,10 +179,13 @@ def _check_worker(rank, world, port, q):
             def release_graph(self):
                 self.released = True
 
+            def resync_state(self, src=0):
+                self.dp.broadcast_tensors([self.p], src=src)
+
         for name, kw in (("ok", {}), ("mismatch", {"mismatch": True}), ("capture_fail", {"fail_capture": True})):
             t = FakeTrainer(**kw)
             graphed, msg = capture_dp_step(t, None, 1, "cpu", log=lambda m: None)
-            res["dp_" + name] = (graphed, t.released, msg)
+            res["dp_" + name] = (graphed, t.released, msg, dp.consistent([t.p]))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -206,4 +209,6 @@ def test_cross_rank_checksum_and_capture_fallback_gloo_world2():
         assert got["dp_ok"][:2] == (True, False), got["dp_ok"]
         # the mismatch branch: both ranks release the graph and run eager steps, whichever differed
         assert got["dp_mismatch"][:2] == (False, True) and "MISMATCH" in got["dp_mismatch"][2], got["dp_mismatch"]
+        # ... and the state the verifying replay left diverged is rank 0's again on every rank
+        assert got["dp_mismatch"][3] is True and got["dp_ok"][3] is True, got["dp_mismatch"]
         assert got["dp_capture_fail"][:2] == (False, True), got["dp_capture_fail"]

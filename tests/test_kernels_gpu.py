@@ -82,10 +82,18 @@ def test_gemm_bf16_g8_ktile_counts(layout, Kd):
         assert err <= (1e-5 if odt == torch.float32 else 8e-3), (odt, err)
 
 
+@pytest.fixture
+def g4_restore():
+    """the four-wave GEMM switches (mmfd_set_g4_mode / _kmax) as they were before the test"""
+    old = K.g4_mode()
+    yield
+    K.set_g4_mode(*old)
+
+
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 128), (768, 2304, 768), (1024, 512, 1024),
                                    (2048, 3072, 768)])
 @pytest.mark.parametrize("with_bias", [False, True])
-def test_gemm_bf16_g4_forward(shape, with_bias, monkeypatch):
+def test_gemm_bf16_g4_forward(shape, with_bias, g4_restore):
     """the four-wave assembly-scheduled forward GEMM (gemm_g4.hip: bf16 -> bf16, K-contiguous
     operands, full 256x256 tiles, bias epilogue) against fp64, and against gemm256_kernel on the same
     inputs (MMFD_G4=0 routes the product there): both accumulate each output's K in the same order
@@ -95,9 +103,9 @@ def test_gemm_bf16_g4_forward(shape, with_bias, monkeypatch):
     B = _rand(N, Kd, dtype=torch.bfloat16, seed=N + 8).to(DEV)
     bias = _rand(N, seed=Kd + 9).to(DEV) if with_bias else None
     ref = A.double().cpu() @ B.double().cpu().T + (bias.double().cpu() if with_bias else 0.0)
-    monkeypatch.setenv("MMFD_G4", "1")
+    K.set_g4_mode("on")
     g4 = K.gemm(A, B, bias=bias)
-    monkeypatch.setenv("MMFD_G4", "0")
+    K.set_g4_mode("off")
     g8 = K.gemm(A, B, bias=bias)
     torch.cuda.synchronize()
     err = (g4.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
@@ -107,8 +115,49 @@ def test_gemm_bf16_g4_forward(shape, with_bias, monkeypatch):
     assert diff <= ulp, (diff, ulp)
 
 
+@pytest.mark.parametrize("Kd", [64, 768])
+@pytest.mark.parametrize("mode", ["bias", "gelu_aux", "dropout_residual"])
+def test_gemm_bf16_g4_strided_views_match_g8(Kd, mode, g4_restore):
+    """the four-wave kernel on column-sliced views — lda / ldb > K (a Q|K|V slice of a
+    packed activation), ldc / ldr / ldaux > N — is bit-identical to gemm256_kernel, K = 64 (one K-tile:
+    the two-tile-ahead prefetch reads past K inside the row's buffer range) included; the bytes of
+    the wider buffers outside the views stay untouched"""
+    M, N = 512, 768
+    A_full = _rand(M, Kd + 128, dtype=torch.bfloat16, seed=61).to(DEV)
+    B_full = _rand(N, Kd + 64, dtype=torch.bfloat16, seed=62).to(DEV)
+    A, B = A_full[:, 64:64 + Kd], B_full[:, 32:32 + Kd]  # 16-B aligned column slices
+    bias = _rand(N, seed=63).to(DEV)
+    res_full = _rand(M, N + 256, dtype=torch.bfloat16, seed=64).to(DEV)
+    res = res_full[:, 128:128 + N]
+    outs = {}
+    for g4 in ("1", "0"):
+        K.set_g4_mode("gelu" if g4 == "1" else "off")
+        c_full = torch.full((M, N + 512), 3.0, dtype=torch.bfloat16, device=DEV)
+        x_full = torch.full((M, N + 128), 5.0, dtype=torch.bfloat16, device=DEV)
+        c, x = c_full[:, 256:256 + N], x_full[:, 64:64 + N]
+        if mode == "bias":
+            K.gemm(A, B, bias=bias, out=c)
+        elif mode == "gelu_aux":
+            K.gemm(A, B, bias=bias, act=K.ACT_GELU, aux=x, out=c)
+        else:
+            K.gemm(A, B, bias=bias, residual=res, dropout_p=0.1, seed=K.Seed(78, device=DEV), salt=6, out=c)
+        outs[g4] = (c_full, x_full)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    assert torch.equal(outs["1"][1], outs["0"][1])
+    c_full, x_full = outs["1"]
+    assert bool((c_full[:, :256] == 3.0).all()) and bool((c_full[:, 256 + N:] == 3.0).all())
+    if mode == "gelu_aux":
+        assert bool((x_full[:, :64] == 5.0).all()) and bool((x_full[:, 64 + N:] == 5.0).all())
+    ref = A.double().cpu() @ B.double().cpu().T + bias.double().cpu()
+    got = outs["1"][1][:, 64:64 + N] if mode == "gelu_aux" else outs["1"][0][:, 256:256 + N]
+    if mode != "dropout_residual":
+        err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= 8e-3, err
+
+
 @pytest.mark.parametrize("mode", ["gelu_aux", "residual", "dropout_residual"])
-def test_gemm_bf16_g4_epilogues_match_g8(mode, monkeypatch):
+def test_gemm_bf16_g4_epilogues_match_g8(mode, g4_restore):
     """the four-wave kernel's fused epilogues of the encoder forward Linears (FFN1: bias + GELU with
     the pre-activation to aux; attention output / FFN2: bias [+ hashed dropout] + residual) are
     bit-identical to gemm256_kernel's on the same inputs"""
@@ -118,9 +167,9 @@ def test_gemm_bf16_g4_epilogues_match_g8(mode, monkeypatch):
     bias = _rand(N, seed=53).to(DEV)
     res = _rand(M, N, dtype=torch.bfloat16, seed=54).to(DEV)
     outs = {}
-    monkeypatch.setenv("MMFD_G4_GELU", "1")  # (the GELU mode is opt-in in the step, see gemm_g4.hip)
     for g4 in ("1", "0"):
-        monkeypatch.setenv("MMFD_G4", g4)
+        # (the GELU mode is opt-in in the step, see gemm_g4.hip)
+        K.set_g4_mode("gelu" if g4 == "1" else "off")
         aux = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
         if mode == "gelu_aux":
             out = K.gemm(A, B, bias=bias, act=K.ACT_GELU, aux=aux)

@@ -34,9 +34,9 @@ for name, M, N, Kd in (("bert qkv", 65536, 2304, 768), ("vit qkv", 100864, 2304,
         else:
             A = (torch.rand(M, Kd, device=dev) * 4 - 2).bfloat16(); B = (torch.rand(N, Kd, device=dev) * 4 - 2).bfloat16()
         bias = torch.randn(N, device=dev)
-        os.environ["MMFD_G4"] = "1"
+        K.set_g4_mode("on")
         g4 = t(lambda: K.gemm(A, B, bias=bias))
-        os.environ["MMFD_G4"] = "0"
+        K.set_g4_mode("off")
         g8 = t(lambda: K.gemm(A, B, bias=bias))
         lib = t(lambda: torch.matmul(A, B.t()))
         print(f"{name:9s} {dist:8s} g4 {g4:7.1f} us  g8 {g8:7.1f} us  hipBLASLt {lib:7.1f} us", flush=True)

@@ -28,7 +28,7 @@ for name, M, N, Kd, mode in (("bert qkv", 65536, 2304, 768, "bias"), ("vit ffn1 
         kw.update(residual=torch.randn(M, N, device=dev, generator=g).bfloat16())
     res = {}
     for g4 in ("1", "0"):
-        os.environ["MMFD_G4"] = g4
+        K.set_g4_mode("on" if g4 == "1" else "off")
         for _ in range(3):
             out = K.gemm(A, B, **kw)
         torch.cuda.synchronize()

@@ -12,7 +12,7 @@ for name, M, N, Kd in (("bert qkv", 65536, 2304, 768), ("bert out", 65536, 768, 
       bias = torch.randn(N, device=dev)
       res = {}
       for g4 in ("1", "0"):
-          os.environ["MMFD_G4"] = g4
+          K.set_g4_mode("on" if g4 == "1" else "off")
           for _ in range(3): K.gemm(A, B, bias=bias)
           torch.cuda.synchronize()
           e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,7 +50,7 @@ for name, M, N, Kd, mode in (("bert ffn1 gelu+aux", 65536, 3072, 768, "gelu"), (
         kw.update(residual=res_t)
     res = {}
     for g4 in ("1", "0"):
-        os.environ["MMFD_G4"] = g4
+        K.set_g4_mode(("gelu" if mode == "gelu" else "on") if g4 == "1" else "off")
         for _ in range(3): K.gemm(A, B, **kw)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -242,17 +242,26 @@ __global__ void __launch_bounds__(256) gemm_g4_kernel(const bf16* __restrict__ A
 namespace mmfd_gemmx {
 // the products the four-wave kernel takes: bf16 x bf16 -> bf16, both operands K-contiguous (the
 // nn.Linear forward), full tiles, alpha 1 and at most a bias in the epilogue; env MMFD_G4=0 sends
-// them to gemm256_kernel (A/B measurements, tests)
+// them to gemm256_kernel (A/B measurements, tests). The switches are read from the environment once,
+// when the library loads (MMFD_G4=0: off; MMFD_G4_GELU=1: the FFN1 GELU mode too; MMFD_G4_KMAX), and
+// changed at run time only through mmfd_set_g4_mode / mmfd_set_g4_kmax — never a getenv per launch
+int g_g4_mode = [] {
+  const char* v = getenv("MMFD_G4");
+  return (v && v[0] == '0') ? 0 : getenv("MMFD_G4_GELU") ? 2 : 1;
+}();
+int64_t g_g4_kmax = [] {
+  const char* k = getenv("MMFD_G4_KMAX");
+  return k ? (int64_t)atoll(k) : (int64_t)1024;
+}();
 bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_t s) {
-  const char* env = getenv("MMFD_G4");
-  if (env && env[0] == '0') return false;
+  const int mode = g_g4_mode;
+  if (mode == 0) return false;
   if (a.dtype != MMFD_BF16 || a.c_dtype != MMFD_BF16 || a.trans_a || a.trans_b || splits > 1) return false;
   if (a.M % 256 || a.N % 256 || a.K % 64 || a.K < 64 || a.alpha != 1.0f || a.beta != 0.0f || a.a_rowsum) return false;
   // K <= 1024: the short-K products (QKV, attention output, FFN1 at K = 768) gain from the register
   // epilogue; at K = 3072 (FFN2) the power-limited main loop is no faster than gemm256_kernel's and
   // ViT's FFN2 measured 10 % slower (profiles/r05_g4_vs_g8_vs_hipblaslt.log)
-  static const int64_t kmax = getenv("MMFD_G4_KMAX") ? atoll(getenv("MMFD_G4_KMAX")) : 1024;  // A/B override
-  if (a.K > kmax) return false;
+  if (a.K > g_g4_kmax) return false;
   if (!e.vec || e.pl || e.beta != 0.0f) return false;
   // the epilogue modes of the encoder forward Linears (anything else runs on gemm256_kernel)
   int epi = -1;
@@ -261,7 +270,7 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   // FFN1 (bias + GELU + pre-activation): measured 0.89-1.03x of gemm256_kernel across boxes (its
   // time is the GELU's VALU work, which one wave per SIMD does not hide better than two;
   // profiles/r05_g4_schedule_ab.log): left on gemm256_kernel unless MMFD_G4_GELU=1
-  else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f && getenv("MMFD_G4_GELU")) epi = 3;
+  else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f && mode == 2) epi = 3;
   if (epi < 0) return false;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al16(a.A) || !al16(a.B) || !al16(a.C)) return false;
@@ -281,6 +290,19 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   return true;
 }
 }  // namespace mmfd_gemmx
+
+extern "C" int mmfd_set_g4_mode(int mode) {
+  MMFD_CHECK_ARG(mode >= -1 && mode <= 2, "mmfd_set_g4_mode: mode %d (-1 query, 0 off, 1 on, 2 on + GELU)", mode);
+  const int old = mmfd_gemmx::g_g4_mode;
+  if (mode >= 0) mmfd_gemmx::g_g4_mode = mode;
+  return old;
+}
+
+extern "C" int64_t mmfd_set_g4_kmax(int64_t kmax) {
+  const int64_t old = mmfd_gemmx::g_g4_kmax;
+  if (kmax > 0) mmfd_gemmx::g_g4_kmax = kmax;
+  return old;
+}
 '''
 
 

@@ -46,7 +46,7 @@ def reads(kc_dst, stage_addr_a, stage_addr_b, kc_src):
     return out
 
 
-def dmas(part):
+def dmas(part, form=0):
     """8 LDS-DMA pieces: 4 into the wave's quarter of the A region, 4 into its quarter of the B
     region of K half `part` (kc0 in part A, kc1 in part B) of the current stage. m0 walks s42 (A) /
     s43 (B). The sources are the real operand rows: piece p of a wave covers 16 rows x 64 B (one K
@@ -56,13 +56,25 @@ def dmas(part):
     for p in range(ND):
         reg, vo, rs = ("s42", "%[voffa]", "%[srda]") if p < 4 else ("s43", "%[voffb]", "%[srdb]")
         step = [f"s_add_u32 s41, s40, {part * 64}"] if p % 4 == 0 else ["s_add_u32 s41, s41, %[pstep]"]
-        out.append([f"s_mov_b32 m0, {reg}"] + step +
-                   [f"buffer_load_dwordx4 {vo}, {rs}, s41 offen lds", f"s_add_u32 {reg}, {reg}, 1024"])
+        if form == 0:
+            out.append([f"s_mov_b32 m0, {reg}"] + step +
+                       [f"buffer_load_dwordx4 {vo}, {rs}, s41 offen lds", f"s_add_u32 {reg}, {reg}, 1024"])
+        elif form == 1:  # no m0 write per piece (m0 set once per part: wrong placement, timing only)
+            out.append(step + [f"buffer_load_dwordx4 {vo}, {rs}, s41 offen lds"])
+        elif form == 2:  # plain 16-B load into a dead VGPR quad (no LDS write)
+            out.append(step + [f"buffer_load_dwordx4 v[132:135], {vo}, {rs}, s41 offen"])
+        elif form == 3:  # 4-B LDS-DMA pieces (256 B per wave instruction)
+            out.append([f"s_mov_b32 m0, {reg}"] + step +
+                       [f"buffer_load_dword {vo}, {rs}, s41 offen lds", f"s_add_u32 {reg}, {reg}, 1024"])
     return out
 
 
-def part(kc, v, rd, dm):
-    """64 MFMAs of K half kc with the reads rd and DMA pieces dm placed per variant v"""
+SHIFT = {5: 2, 6: 1, 7: 2, 8: 0, 9: 0, 10: 0}
+FORM = {8: 1, 9: 2, 10: 3}  # per-wave DMA slot stagger (variants 5-7), in MFMAs
+
+
+def part(kc, v, rd, dm, w=0):
+    """64 MFMAs of K half kc with the reads rd and DMA pieces dm placed per variant v (wave w)"""
     mf = [mfma(i, j, kc) for i in range(8) for j in range(8)]
     lines = []
     if v == 3:  # bursts first
@@ -73,17 +85,21 @@ def part(kc, v, rd, dm):
         return lines
     ri = di = 0
     ra, da = int(os.environ.get("G4_READ_AT", "0")), int(os.environ.get("G4_DMA_AT", "2"))  # schedule A/B
+    if v >= 5:
+        da = (da + w * SHIFT[v]) % 8
+        if v == 7:
+            ra = (ra + w) % 4
     for k, m in enumerate(mf):
         lines.append(m)
         if v >= 1 and k % 4 == ra and ri < len(rd):
             lines.append(rd[ri]); ri += 1
-        if v in (2, 4) and k % 8 == da and di < len(dm):
+        if v in (2, 4, 5, 6, 7, 8, 9, 10) and k % 8 == da and di < len(dm):
             lines += dm[di]; di += 1
     assert ri == len(rd) and di == len(dm)
     return lines
 
 
-def kernel(v):
+def kernel(v, w=0):
     L = []
     # prologue: zero the accumulators, DMA iterations 0 (stage 0) and 1 (stage 1), wait for 0's kc0
     L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
@@ -92,7 +108,7 @@ def kernel(v):
         for half in (0, 1):
             L += [f"s_add_u32 s42, %[mA], {st * 65536 + half * 16384}", f"s_add_u32 s43, %[mB], {st * 65536 + half * 16384}"]
             if v >= 2:
-                for d in dmas(half):
+                for d in dmas(half, FORM.get(v, 0)):
                     L += d
         L += ["s_add_u32 s40, s40, 128"]
     if v >= 2:
@@ -105,6 +121,8 @@ def kernel(v):
     L += ["s_waitcnt vmcnt(16) lgkmcnt(0)" if v >= 2 else "s_waitcnt lgkmcnt(0)", "s_barrier"]
     L += ["s_cmp_eq_u32 s45, 0"]
     L += ["s_cselect_b32 s42, %[mA], %[mA1]", "s_cselect_b32 s43, %[mB], %[mB1]"]
+    if v == 8:
+        L += ["s_mov_b32 m0, s42"]
     # part A: kc1 reads of stage t%2 (address registers chosen by branch-free selects would need a
     # VGPR select; the two stages are two code paths instead)
     body = {}
@@ -112,13 +130,15 @@ def kernel(v):
         rA, rB = ("%[rA0]", "%[rB0]") if st == 0 else ("%[rA1]", "%[rB1]")
         nA, nB = ("%[rA1]", "%[rB1]") if st == 0 else ("%[rA0]", "%[rB0]")
         rdA = reads(1, rA, rB, 1) if v >= 1 else []
-        dmA = dmas(0) if v >= 2 else []
-        pa = part(0, v, rdA, dmA)
+        dmA = dmas(0, FORM.get(v, 0)) if v >= 2 else []
+        pa = part(0, v, rdA, dmA, w)
         mid = ["s_waitcnt vmcnt(16) lgkmcnt(0)" if v >= 2 else "s_waitcnt lgkmcnt(0)", "s_barrier"]
         mid += [f"s_add_u32 s42, %[mA{'' if st == 0 else '1'}], 16384", f"s_add_u32 s43, %[mB{'' if st == 0 else '1'}], 16384"]
         rdB = reads(0, nA, nB, 0) if v >= 1 else []
-        dmB = dmas(1) if v >= 2 else []
-        pb = part(1, v, rdB, dmB)
+        dmB = dmas(1, FORM.get(v, 0)) if v >= 2 else []
+        if v == 8:
+            mid.append("s_mov_b32 m0, s42")
+        pb = part(1, v, rdB, dmB, w)
         body[st] = pa + mid + pb
     L += ["s_cbranch_scc0 L_odd_%="]
     L += body[0]
@@ -142,13 +162,14 @@ def kernel(v):
 
 
 def emit():
-    clob = [f'"v{r}"' for r in range(4, 132)] + [f'"a{r}"' for r in range(256)] + \
+    clob = [f'"v{r}"' for r in range(4, 136)] + [f'"a{r}"' for r in range(256)] + \
            [f'"s{r}"' for r in range(40, 47)] + ['"m0"', '"scc"', '"memory"']
     parts = []
-    for v in range(5):
-        asm = "\\n\\t".join(kernel(v))
+    for v, w in [(v, 0) for v in range(5)] + [(v, w) for v in (5, 6, 7, 8, 9, 10) for w in range(4)]:
+        asm = "\\n\\t".join(kernel(v, w))
+        name = f"loop<{v}>" if v < 5 else f"loopw<{v}, {w}>"
         parts.append(f"""
-template <> __device__ __forceinline__ void loop<{v}>(const LoopArgs& x) {{
+template <> __device__ __forceinline__ void {name}(const LoopArgs& x) {{
   asm volatile("{asm}"
       :
       : [voffa] "v"(x.voffa), [voffb] "v"(x.voffb), [srda] "s"(x.srda), [srdb] "s"(x.srdb), [nit] "s"(x.nit),
@@ -180,6 +201,7 @@ struct LoopArgs {
   uint32_t ldc2, ldc2x12;              // output row pitch in bytes, and 12 rows of it
 };
 template <int V> __device__ void loop(const LoopArgs& x);
+template <int V, int W> __device__ void loopw(const LoopArgs& x);  // per-wave schedules (V >= 5)
 '''
 
 FOOTER = r'''
@@ -220,7 +242,11 @@ __global__ void __launch_bounds__(256) g4loop_kernel(const __bf16* A, const __bf
   x.voffc = (((wave >> 1) * 128u + 4u * (lane >> 4)) * ldc + (wave & 1) * 128u + 8u * (lane & 15)) * 2u;
   __syncthreads();
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  loop<V>(x);
+  if constexpr (V < 5) loop<V>(x);
+  else if (wave == 0) loopw<V, 0>(x);
+  else if (wave == 1) loopw<V, 1>(x);
+  else if (wave == 2) loopw<V, 2>(x);
+  else loopw<V, 3>(x);
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0 && blockIdx.x < 4096) ticks[blockIdx.x * 4 + wave] = t1 - t0;
 }
@@ -289,6 +315,12 @@ int main(int argc, char** argv) {
       run<2>("V2 MFMA + reads + DMA, spread", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
       run<3>("V3 MFMA + reads + DMA, bursts", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
       run<4>("V4 = V2 + register epilogue", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<5>("V5 = V2, DMA slot +2 MFMAs per wave", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<6>("V6 = V2, DMA slot +1 MFMA per wave", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<7>("V7 = V5, reads +1 MFMA per wave", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<8>("V8 = V2, no m0 write per piece", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<9>("V9 = V2, plain 16-B loads (no LDS)", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
+      run<10>("V10 = V2, 4-B LDS-DMA pieces", s.name, A, B, s.M, s.N, s.K, xg, ticks, out);
     }
   hipError_t err = hipDeviceSynchronize();
   printf("status: %s\n", hipGetErrorString(err));
