@@ -81,6 +81,19 @@ typedef struct mmfd_epilogue {
                               (beta = 0): a GEMM output whose only consumers are split-operand GEMMs */
 } mmfd_epilogue;
 
+/* Implicit-GEMM convolution geometry (mmfd_gemm_args.conv; the ResNet50 extractor's convolutions,
+   im2im_retrieval.py:14-17, 29-36): A is the NHWC activation x[N][H][W][C] and
+     op(A)[m][k] = x[n][oh*stride - pad + kh][ow*stride - pad + kw][c]   (0 outside the image)
+   with m = (n*Ho + oh)*Wo + ow, k = (kh*KW + kw)*C + c — the im2col matrix, gathered by the GEMM's
+   operand fill instead of being written. Requires trans_a = 0, M = N*Ho*Wo, K = KH*KW*C, C a
+   multiple of 32 (fp32) / 64 (bf16), x 16-B aligned, no a_rowsum; lda is ignored. With fp32
+   operands on the split-operand path a_planes, when given, are the planes [3][N*H*W][C] of x. */
+typedef struct mmfd_conv_geom {
+  int64_t N, H, W, C;      /* input images */
+  int KH, KW, stride, pad;
+  int64_t Ho, Wo;          /* output size */
+} mmfd_conv_geom;
+
 typedef struct mmfd_gemm_args {
   int64_t struct_size;     /* = sizeof(mmfd_gemm_args) of the caller's header; the library refuses
                               any other value (MMFD_ERR_INVALID): a caller built against another
@@ -108,6 +121,8 @@ typedef struct mmfd_gemm_args {
   /* 1: the fp32 A / B was never written (its only form is the planes): mmfd_gemm fails with
      MMFD_ERR_UNSUPPORTED instead of reading it when the split-operand path is not taken */
   int a_planes_only, b_planes_only;
+  /* ABI 3: non-NULL = A is an implicit convolution operand (mmfd_conv_geom above) */
+  const mmfd_conv_geom* conv;
 } mmfd_gemm_args;
 
 int mmfd_gemm(const mmfd_gemm_args* args, mmfd_stream_t stream);

@@ -58,24 +58,32 @@ __global__ void im2col_nhwc_kernel(int64_t N, int64_t H, int64_t W, int64_t C, i
   }
 }
 
-// stem im2col straight from the fp32 NCHW pixel tensor (C = 3): out[row][(kh*KW + kw)*C + c]
+// stem im2col straight from the fp32 NCHW pixel tensor (C = 3): out[row][(kh*KW + kw)*C + c]. One
+// thread per (output row, kh): its KW*C outputs are contiguous (the KH threads of a row write one
+// contiguous K row), its loads are KW consecutive pixels of each channel row; 32-bit index math (the
+// host checks the sizes), the K padding columns written by the kh = KH-1 thread. (The first form —
+// one thread per output element with 64-bit divisions for every index — ran at ~0.9 TB/s.)
 template <typename T>
-__global__ void im2col_nchw_kernel(int64_t N, int64_t C, int64_t H, int64_t W, int KH, int KW, int stride, int pad,
-                                   int64_t Ho, int64_t Wo, int64_t Kpad, const float* __restrict__ x,
-                                   T* __restrict__ out) {
-  const int64_t n_total = N * Ho * Wo * Kpad;
-  const int64_t kreal = (int64_t)KH * KW * C;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / Kpad, k = i % Kpad;
-    float v = 0.f;
-    if (k < kreal) {
-      const int64_t c = k % C, kk = k / C;
-      const int kw = (int)(kk % KW), kh = (int)(kk / KW);
-      const int64_t wo = row % Wo, t = row / Wo, ho = t % Ho, nimg = t / Ho;
-      const int64_t hi = ho * stride - pad + kh, wi = wo * stride - pad + kw;
-      if (hi >= 0 && hi < H && wi >= 0 && wi < W) v = x[((nimg * C + c) * H + hi) * W + wi];
+__global__ void __launch_bounds__(256) im2col_nchw_kernel(uint32_t N, uint32_t C, uint32_t H, uint32_t W, uint32_t KH,
+                                                          uint32_t KW, uint32_t stride, uint32_t pad, uint32_t Ho,
+                                                          uint32_t Wo, uint32_t Kpad, const float* __restrict__ x,
+                                                          T* __restrict__ out) {
+  const uint32_t total = N * Ho * Wo * KH;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t row = i / KH, kh = i - row * KH;
+    const uint32_t wo = row % Wo, t = row / Wo, ho = t % Ho, n = t / Ho;
+    const int hi = (int)(ho * stride + kh) - (int)pad;
+    const int wi0 = (int)(wo * stride) - (int)pad;
+    T* o = out + (size_t)row * Kpad + kh * KW * C;
+    const bool hin = hi >= 0 && hi < (int)H;
+    for (uint32_t kw = 0; kw < KW; ++kw) {
+      const int wi = wi0 + (int)kw;
+      const bool in = hin && wi >= 0 && wi < (int)W;
+      for (uint32_t c = 0; c < C; ++c)
+        o[kw * C + c] = from_f32<T>(in ? x[((size_t)(n * C + c) * H + (uint32_t)hi) * W + (uint32_t)wi] : 0.f);
     }
-    out[i] = from_f32<T>(v);
+    if (kh == KH - 1)
+      for (uint32_t k = KH * KW * C; k < Kpad; ++k) out[(size_t)row * Kpad + k] = from_f32<T>(0.f);
   }
 }
 
@@ -175,15 +183,19 @@ extern "C" int mmfd_im2col_nchw(int dtype, int64_t N, int64_t C, int64_t H, int6
                                 int pad, int64_t Ho, int64_t Wo, int64_t Kpad, const float* x, void* out,
                                 mmfd_stream_t stream) {
   MMFD_CHECK_ARG(Kpad >= (int64_t)KH * KW * C, "im2col_nchw: Kpad too small");
-  const int64_t n = N * Ho * Wo * Kpad;
+  MMFD_CHECK_ARG(N * C * H * W < (1ll << 32) && N * Ho * Wo * KH < (1ll << 32) && KH > 0 && KW > 0 && stride > 0,
+                 "im2col_nchw: sizes past the 32-bit index range");
+  const int64_t n = N * Ho * Wo * KH;
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMFD_BF16)
-    hipLaunchKernelGGL((im2col_nchw_kernel<bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, N, C, H, W, KH, KW, stride, pad,
-                       Ho, Wo, Kpad, x, (bf16*)out);
+    hipLaunchKernelGGL((im2col_nchw_kernel<bf16>), dim3(grid_for(n, 256)), dim3(256), 0, s, (uint32_t)N, (uint32_t)C,
+                       (uint32_t)H, (uint32_t)W, (uint32_t)KH, (uint32_t)KW, (uint32_t)stride, (uint32_t)pad, (uint32_t)Ho,
+                       (uint32_t)Wo, (uint32_t)Kpad, x, (bf16*)out);
   else
-    hipLaunchKernelGGL((im2col_nchw_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, N, C, H, W, KH, KW, stride,
-                       pad, Ho, Wo, Kpad, x, (float*)out);
+    hipLaunchKernelGGL((im2col_nchw_kernel<float>), dim3(grid_for(n, 256)), dim3(256), 0, s, (uint32_t)N, (uint32_t)C,
+                       (uint32_t)H, (uint32_t)W, (uint32_t)KH, (uint32_t)KW, (uint32_t)stride, (uint32_t)pad, (uint32_t)Ho,
+                       (uint32_t)Wo, (uint32_t)Kpad, x, (float*)out);
   MMFD_CHECK_LAUNCH("im2col_nchw");
   return 0;
 }

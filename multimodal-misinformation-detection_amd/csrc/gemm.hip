@@ -22,11 +22,14 @@
 
 namespace {
 
-template <typename T, int TA, int TB, typename TC>
-__global__ void __launch_bounds__(NT, 1)
-gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
-                 TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
-                 int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
+// CONV: implicit-GEMM convolution (ConvGeom): A is the NHWC activation and its fill gathers the
+// im2col rows per K-tile (ConvFill); TA = 0 only. The body is shared by gemm_mfma_kernel and
+// conv_mfma_kernel (two kernel names, so the plain GEMM's name in traces stays what it was)
+template <typename T, int TA, int TB, typename TC, bool CONV>
+__device__ __forceinline__ void
+gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+               TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
+               int64_t K, float alpha, int tiles_per_split, const EpiArgs& e, const ConvGeom& cg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int APIECES = A_BYTES / 1024 / NWAVES;  // 4 pieces per wave
   constexpr int BPIECES = B_BYTES / 1024 / NWAVES;  // 2 pieces per wave
@@ -51,18 +54,22 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (TA == 0 ? M : K) * lda * (int64_t)sizeof(T));
+  const int64_t a_bytes = CONV ? cg.H * cg.W * cg.C * (M / (cg.Ho * cg.Wo)) * (int64_t)sizeof(T)
+                               : (TA == 0 ? M : K) * lda * (int64_t)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, a_bytes);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * (int64_t)sizeof(T));
-  Fill<T, TA, BM, APIECES> fa;
+  std::conditional_t<CONV, ConvFill<T, APIECES>, Fill<T, TA, BM, APIECES>> fa;
   Fill<T, TB, BN, BPIECES> fb;
-  fa.init(lda, m0, M, wave, lane);
+  if constexpr (CONV) fa.init(cg, m0, M, wave, lane);
+  else fa.init(lda, m0, M, wave, lane);
   fb.init(ldb, n0, N, wave, lane);
 
   auto issue = [&](int t) {
     const int64_t k0 = (int64_t)(kt0 + t) * GT<T>::BK;
     const bool tail = k0 + GT<T>::BK > K;
     char* st = smem + (t % NSTAGE) * STAGE_BYTES;
-    fa.issue(rsa, st, (uint32_t)(k0 * (TA == 0 ? 1 : lda) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
+    if constexpr (CONV) fa.issue(rsa, st, cg, k0, K, wave);
+    else fa.issue(rsa, st, (uint32_t)(k0 * (TA == 0 ? 1 : lda) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
     fb.issue(rsb, st + A_BYTES, (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
   };
 
@@ -144,6 +151,22 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
   }
 }
 
+
+template <typename T, int TA, int TB, typename TC>
+__global__ void __launch_bounds__(NT, 1)
+gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                 TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
+                 int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
+  gemm_mfma_body<T, TA, TB, TC, false>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, ConvGeom{});
+}
+// implicit-GEMM convolution on the 256x128 kernel (mmfd_gemm_args.conv): A = the NHWC activation
+template <typename T, typename TC>
+__global__ void __launch_bounds__(NT, 1)
+conv_mfma_kernel(const T* __restrict__ X, const T* __restrict__ B, int64_t ldb, TC* __restrict__ C, int64_t ldc,
+                 float* __restrict__ ws, int64_t M, int64_t N, int64_t K, float alpha, int tiles_per_split, EpiArgs e,
+                 ConvGeom cg) {
+  gemm_mfma_body<T, 0, 0, TC, true>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, cg);
+}
 
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
@@ -227,6 +250,18 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
   hipLaunchKernelGGL((gemm_mfma_kernel<T, TA, TB, TC>), grid, dim3(NT), LDS_BYTES, s,
                      (const T*)a.A, a.lda, (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K,
                      a.alpha, tps, e);
+}
+template <typename T, typename TC>
+void launch_conv_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s,
+                      const ConvGeom& cg) {
+  dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_mfma_kernel<T, TC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((conv_mfma_kernel<T, TC>), grid, dim3(NT), LDS_BYTES, s, (const T*)a.A, (const T*)a.B, a.ldb,
+                     (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, cg);
 }
 
 
@@ -344,6 +379,12 @@ void dispatch_layout(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int s
 bool mfma_ok(const mmfd_gemm_args& a) {
   const int epc = (a.dtype == MMFD_BF16) ? 8 : 4;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (a.conv) {  // implicit convolution: checked by conv_geom(); B as below
+    const int64_t esz = a.dtype == MMFD_BF16 ? 2 : 4;
+    const int64_t bbytes = (a.trans_b ? a.K : a.N) * a.ldb * esz;
+    return al16(a.B) && a.ldb % epc == 0 && (a.trans_b ? a.N : a.K) % epc == 0 && a.N >= 16 &&
+           bbytes < (1ll << 31) - 4096;
+  }
   if (!al16(a.A) || !al16(a.B)) return false;
   if (a.lda % epc || a.ldb % epc) return false;
   const int64_t a_ext = a.trans_a ? a.M : a.K;  // contiguous extent
@@ -406,6 +447,9 @@ X6Plan x6_plan(const mmfd_gemm_args& a) {
   X6Plan p{};
   if (g_fp32_mode != 1 || a.dtype != MMFD_F32 || a.c_dtype != MMFD_F32 || !use_g8(a)) return p;
   p.rows_a = a.trans_a ? a.K : a.M; p.cols_a = a.trans_a ? a.M : a.K;
+  if (a.conv) {  // the planes of the NHWC activation, not of the (never written) im2col matrix
+    p.rows_a = a.conv->N * a.conv->H * a.conv->W; p.cols_a = a.conv->C;
+  }
   p.rows_b = a.trans_b ? a.K : a.N; p.cols_b = a.trans_b ? a.N : a.K;
   if (p.cols_a % 8 || p.cols_b % 8) return p;
   if ((a.trans_a || a.trans_b) && a.K % (x6_fused() ? 32 : 64)) return p;
@@ -434,6 +478,28 @@ int rowsum_fallback(const mmfd_gemm_args& a, void* ws, int64_t ws_bytes, hipStre
   if (!a.trans_a)
     return mmfd_set_error(MMFD_ERR_UNSUPPORTED, "mmfd_gemm: a_rowsum without trans_a needs the bf16 MFMA path");
   return mmfd_colsum(a.dtype, a.K, a.M, a.A, a.lda, a.a_rowsum, a.a_rowsum_beta, ws, ws_bytes, s);
+}
+
+// the implicit-convolution geometry of `a` (on = 0 without one), or an error string
+const char* conv_geom(const mmfd_gemm_args& a, ConvGeom& g) {
+  g = ConvGeom{};
+  if (!a.conv) return nullptr;
+  const mmfd_conv_geom& c = *a.conv;
+  const int64_t kstep = a.dtype == MMFD_BF16 ? 64 : 32;  // K per K-tile / split-operand K-step
+  if (a.trans_a) return "conv needs trans_a = 0";
+  if (c.N <= 0 || c.H <= 0 || c.W <= 0 || c.C <= 0 || c.KH <= 0 || c.KW <= 0 || c.stride <= 0 || c.pad < 0)
+    return "conv: bad geometry";
+  if (c.Ho != (c.H + 2 * c.pad - c.KH) / c.stride + 1 || c.Wo != (c.W + 2 * c.pad - c.KW) / c.stride + 1)
+    return "conv: Ho / Wo do not match H, W, KH, KW, stride, pad";
+  if (a.M != c.N * c.Ho * c.Wo || a.K != (int64_t)c.KH * c.KW * c.C) return "conv: M != N*Ho*Wo or K != KH*KW*C";
+  if (c.C % kstep) return "conv: C must be a multiple of 32 (fp32) / 64 (bf16)";
+  if (((uintptr_t)a.A & 15) != 0) return "conv: x must be 16-B aligned";
+  if (a.a_rowsum || a.a_planes_only) return "conv: no a_rowsum / a_planes_only";
+  const int64_t esz = a.dtype == MMFD_BF16 ? 2 : 4;
+  if (c.N * c.H * c.W * c.C * esz >= (1ll << 31) - 4096) return "conv: activation >= 2 GB";
+  g.on = 1; g.KW = c.KW; g.stride = c.stride; g.pad = c.pad;
+  g.H = c.H; g.W = c.W; g.C = c.C; g.Ho = c.Ho; g.Wo = c.Wo;
+  return nullptr;
 }
 
 }  // namespace
@@ -524,6 +590,10 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   }
 
   const bool bf = a.dtype == MMFD_BF16, cbf = a.c_dtype == MMFD_BF16;
+  ConvGeom cg;
+  if (const char* why = conv_geom(a, cg)) return mmfd_set_error(MMFD_ERR_INVALID, "mmfd_gemm: %s", why);
+  if (cg.on && !mfma_ok(a))
+    return mmfd_set_error(MMFD_ERR_UNSUPPORTED, "mmfd_gemm: conv with an unaligned / oversized B operand");
   // an operand whose fp32 copy was never written can only be read through its planes: refuse every
   // path that would read the fp32 copy (the simple kernel below included)
   if ((a.a_planes_only || a.b_planes_only) && (!mfma_ok(a) || !x6_plan(a).on))
@@ -589,7 +659,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     const bf16* pa = (const bf16*)a.a_planes;
     const bf16* pb = (const bf16*)a.b_planes;
     if (!pa) {
-      launch_split3((const float*)a.A, a.lda, xp.rows_a, xp.cols_a, (bf16*)planes, s);
+      launch_split3((const float*)a.A, cg.on ? cg.C : a.lda, xp.rows_a, xp.cols_a, (bf16*)planes, s);
       pa = (const bf16*)planes;
       planes += align256(3 * xp.pa);
     }
@@ -599,11 +669,16 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
     }
     MMFD_CHECK_LAUNCH("split3");
     if (xf) {
-      dispatch_x6f(a, e, ws, splits, tps, rs_out, rs_mode, s, pa, pb, X6Args{nkt, (uint32_t)xp.pa, (uint32_t)xp.pb});
+      dispatch_x6f(a, e, ws, splits, tps, rs_out, rs_mode, s, pa, pb, X6Args{nkt, (uint32_t)xp.pa, (uint32_t)xp.pb}, cg);
+    } else if (cg.on) {
+      return mmfd_set_error(MMFD_ERR_UNSUPPORTED, "mmfd_gemm: conv on the segmented split-operand kernel");
     } else {
       const X6Args x6{(int)((a.K + 63) / 64), (uint32_t)xp.pa, (uint32_t)xp.pb};
       dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s, &x6, pa, pb);
     }
+  } else if (cg.on) {  // implicit convolution: the 256x128 kernel with the window-gathering A fill
+    if (bf) { if (cbf) launch_conv_mfma<bf16, bf16>(a, e, ws, splits, tps, s, cg); else launch_conv_mfma<bf16, float>(a, e, ws, splits, tps, s, cg); }
+    else { if (cbf) launch_conv_mfma<float, bf16>(a, e, ws, splits, tps, s, cg); else launch_conv_mfma<float, float>(a, e, ws, splits, tps, s, cg); }
   } else if (g8 && bf && cbf && !ws && mmfd_gemmx::launch_g4(a, e, splits, s)) {
   } else if (g8 && bf) { if (cbf) dispatch_g8<bf16, bf16>(a, e, ws, splits, tps, rs_out, rs_mode, s); else dispatch_g8<bf16, float>(a, e, ws, splits, tps, rs_out, rs_mode, s); }
   else if (g8) dispatch_g8<float, float>(a, e, ws, splits, tps, rs_out, rs_mode, s);

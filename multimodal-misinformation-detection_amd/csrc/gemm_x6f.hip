@@ -220,12 +220,15 @@ __device__ __forceinline__ float xf_sum3(uint4 h, uint4 m, uint4 l) {
   return (g8_sum16b<bf16>(h) + g8_sum16b<bf16>(m)) + g8_sum16b<bf16>(l);
 }
 
-template <int TA, int TB>
-__global__ void __launch_bounds__(NT, 1)
-gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
-                   float* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
-                   float alpha, int steps_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
-                   int rs_mode, X6Args x6) {
+// CONV: implicit-GEMM convolution (ConvGeom): A is the planes [3][N*H*W][C] of the NHWC activation,
+// its fill gathers the im2col rows per K-step (XfConvFill); TA = 0 only. The body is shared by
+// gemm256_x6f_kernel and conv_x6f_kernel (the plain GEMM keeps its kernel name in traces)
+template <int TA, int TB, bool CONV>
+__device__ __forceinline__ void
+x6f_body(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+         float* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
+         float alpha, int steps_per_split, const EpiArgs& e, float* __restrict__ rs_out, float rs_beta,
+         int rs_mode, const X6Args& x6, const ConvGeom& cg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -257,10 +260,15 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 
   const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, 3 * (int64_t)x6.pa);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, 3 * (int64_t)x6.pb);
-  XfFill<TA> fa0, fa1;
+  std::conditional_t<CONV, XfConvFill, XfFill<TA>> fa0, fa1;
   XfFill<TB> fb0, fb1;
-  fa0.init(lda, m0, M, wave, lane);
-  fa1.init(lda, m0 + 128, M, wave, lane);
+  if constexpr (CONV) {
+    fa0.init(cg, m0, M, wave, lane);
+    fa1.init(cg, m0 + 128, M, wave, lane);
+  } else {
+    fa0.init(lda, m0, M, wave, lane);
+    fa1.init(lda, m0 + 128, M, wave, lane);
+  }
   fb0.init(ldb, n0, N, wave, lane);
   fb1.init(ldb, n0 + 128, N, wave, lane);
 
@@ -273,11 +281,19 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
   auto issue = [&](int h, int t) {
     const int64_t k0 = (int64_t)(st0 + t) * XF_BK;
     char* s = slot(h, t);
-    if (h < 2) {
-      const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * 2);
-      const XfFill<TA>& f = h == 0 ? fa0 : fa1;
+    if (h < 2 && CONV) {
+      if constexpr (CONV) {  // the window gather: one offset per lane for the three planes
+        const uint32_t o = (h == 0 ? fa0 : fa1).off(cg, k0, K);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) f.issue(rsa, s + p * XF_SLOT, so + (uint32_t)p * x6.pa, k0, K, wave);
+        for (int p = 0; p < 3; ++p) dma16(rsa, s + p * XF_SLOT + wave * 1024, o, (uint32_t)p * x6.pa);
+      }
+    } else if (h < 2) {
+      if constexpr (!CONV) {
+        const uint32_t so = (uint32_t)(k0 * (TA == 0 ? 1 : lda) * 2);
+        const XfFill<TA>& f = h == 0 ? fa0 : fa1;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f.issue(rsa, s + p * XF_SLOT, so + (uint32_t)p * x6.pa, k0, K, wave);
+      }
     } else {
       const uint32_t so = (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * 2);
       const XfFill<TB>& f = h == 2 ? fb0 : fb1;
@@ -437,6 +453,23 @@ gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restri
 #undef XF_ROWSUM
 }
 
+template <int TA, int TB>
+__global__ void __launch_bounds__(NT, 1)
+gemm256_x6f_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+                   float* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
+                   float alpha, int steps_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
+                   int rs_mode, X6Args x6) {
+  x6f_body<TA, TB, false>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, steps_per_split, e, rs_out, rs_beta, rs_mode, x6,
+                          ConvGeom{});
+}
+// implicit-GEMM convolution on split operands (mmfd_gemm_args.conv): X = the activation's planes
+__global__ void __launch_bounds__(NT, 1)
+conv_x6f_kernel(const bf16* __restrict__ X, const bf16* __restrict__ B, int64_t ldb, float* __restrict__ C,
+                int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K, float alpha, int steps_per_split,
+                EpiArgs e, X6Args x6, ConvGeom cg) {
+  x6f_body<0, 0, true>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, steps_per_split, e, nullptr, 0.f, 0, x6, cg);
+}
+
 
 
 }  // namespace
@@ -462,9 +495,21 @@ void launch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits
   hipLaunchKernelGGL((gemm256_x6f_kernel<TA, TB>), grid, dim3(NT), G8_LDS, s, (const bf16*)pa, lda, (const bf16*)pb,
                      ldb, (float*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, sps, e, rs_out, a.a_rowsum_beta, rs_mode, x6);
 }
+void launch_conv_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, hipStream_t s,
+                     const void* pa, const void* pb, X6Args x6, const ConvGeom& cg) {
+  dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x6f_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(conv_x6f_kernel, grid, dim3(NT), G8_LDS, s, (const bf16*)pa, (const bf16*)pb, a.K, (float*)a.C,
+                     a.ldc, ws, a.M, a.N, a.K, a.alpha, sps, e, x6, cg);
+}
 void dispatch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int sps, float* rs_out,
-                  int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6) {
-  if (!a.trans_a && !a.trans_b) launch_x6f<0, 0>(a, e, ws, splits, sps, rs_out, rs_mode, s, pa, pb, x6);
+                  int rs_mode, hipStream_t s, const void* pa, const void* pb, X6Args x6, const ConvGeom& cg) {
+  if (cg.on) launch_conv_x6f(a, e, ws, splits, sps, s, pa, pb, x6, cg);
+  else if (!a.trans_a && !a.trans_b) launch_x6f<0, 0>(a, e, ws, splits, sps, rs_out, rs_mode, s, pa, pb, x6);
   else if (!a.trans_a && a.trans_b) launch_x6f<0, 1>(a, e, ws, splits, sps, rs_out, rs_mode, s, pa, pb, x6);
   else if (a.trans_a && !a.trans_b) launch_x6f<1, 0>(a, e, ws, splits, sps, rs_out, rs_mode, s, pa, pb, x6);
   else launch_x6f<1, 1>(a, e, ws, splits, sps, rs_out, rs_mode, s, pa, pb, x6);

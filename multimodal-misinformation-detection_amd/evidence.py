@@ -230,20 +230,34 @@ def _round_up(x, m):
     return (x + m - 1) // m * m
 
 
+# the 3x3 and strided 1x1 convolutions as implicit GEMMs (the GEMM's operand fill gathers the
+# windows; no im2col matrix); MMFD_CONV_IM2COL=1 restores the explicit im2col + GEMM (A/B runs)
+IMPLICIT_CONV = os.environ.get("MMFD_CONV_IM2COL") != "1"
+
+
+def _conv(x, N, H, W, C, w, b, k, s, pad, act=K.ACT_NONE):
+    """conv(k x k, stride s, pad) of NHWC rows x [N*H*W, C] with the folded weight w [Cout, k*k*C]:
+    implicit GEMM where the channel count allows it, else im2col + GEMM. Returns (y, Ho, Wo)."""
+    if IMPLICIT_CONV and K.conv_implicit_ok(x.dtype, C) and w.shape[1] == k * k * C:
+        return K.conv2d_nhwc(x, N, H, W, C, w, k, s, pad, bias=b, act=act)
+    cols, Ho, Wo = K.im2col_nhwc(x, N, H, W, C, k, s, pad, Kpad=w.shape[1])
+    return K.gemm(cols, w, bias=b, act=act), Ho, Wo
+
+
 def _bottleneck(x, N, H, W, blk):
     """relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + shortcut(x)) on NHWC rows"""
     s, planes, cin = blk["stride"], blk["planes"], blk["cin"]
     w1, b1 = blk["c1"]
     h1 = K.gemm(x, w1, bias=b1, act=K.ACT_RELU)                          # 1x1
-    cols, Ho, Wo = K.im2col_nhwc(h1, N, H, W, planes, 3, s, 1)
-    del h1
     w2, b2 = blk["c2"]
-    h2 = K.gemm(cols, w2, bias=b2, act=K.ACT_RELU)                       # 3x3 (stride s)
-    del cols
+    h2, Ho, Wo = _conv(h1, N, H, W, planes, w2, b2, 3, s, 1, act=K.ACT_RELU)  # 3x3 (stride s)
+    del h1
     if blk["ds"] is not None:
         wd, bd = blk["ds"]
-        src = x if s == 1 else K.im2col_nhwc(x, N, H, W, cin, 1, s, 0)[0]
-        ident = K.gemm(src, wd, bias=bd)                                  # 1x1 (stride s) + BN
+        if s == 1:
+            ident = K.gemm(x, wd, bias=bd)                                # 1x1 + BN
+        else:
+            ident = _conv(x, N, H, W, cin, wd, bd, 1, s, 0)[0]            # 1x1 stride s + BN
     else:
         ident = x
     w3, b3 = blk["c3"]

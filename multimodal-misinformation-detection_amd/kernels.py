@@ -74,7 +74,15 @@ class GemmArgs(_Sized):
         ("a_rowsum", ctypes.c_void_p), ("a_rowsum_beta", ctypes.c_float),
         ("a_planes", ctypes.c_void_p), ("b_planes", ctypes.c_void_p),
         ("a_planes_only", ctypes.c_int), ("b_planes_only", ctypes.c_int),
+        ("conv", ctypes.c_void_p),  # const mmfd_conv_geom* (ABI 3): implicit-GEMM convolution
     ]
+
+
+class ConvGeomArgs(ctypes.Structure):
+    """include/mmfd.h mmfd_conv_geom"""
+    _fields_ = [("N", ctypes.c_int64), ("H", ctypes.c_int64), ("W", ctypes.c_int64), ("C", ctypes.c_int64),
+                ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("stride", ctypes.c_int), ("pad", ctypes.c_int),
+                ("Ho", ctypes.c_int64), ("Wo", ctypes.c_int64)]
 
 
 class AttnArgs(_Sized):
@@ -897,6 +905,75 @@ def im2col_nchw(x, k, stride, pad, Kpad, dtype):
     out = torch.empty((N * Ho * Wo, Kpad), device=x.device, dtype=dtype)
     _check(lib().mmfd_im2col_nchw(dtype_code(dtype), N, C, H, W, k, k, stride, pad, Ho, Wo, Kpad,
                                   _ptr(x.contiguous()), _ptr(out), _stream()), "mmfd_im2col_nchw")
+    return out, Ho, Wo
+
+
+def conv_implicit_ok(dtype, C):
+    """whether a convolution over C input channels can run as an implicit GEMM (conv2d_nhwc): a
+    K-tile / split-operand K-step (64 bf16 / 32 fp32 channels) must not straddle two filter taps"""
+    return C % (64 if dtype == torch.bfloat16 else 32) == 0
+
+
+def conv2d_nhwc(x, N, H, W, C, w, k, stride, pad, bias=None, act=ACT_NONE, residual=None, residual_first=False,
+                x_planes=None):
+    """Implicit-GEMM convolution (mmfd_gemm_args.conv): x = the NHWC activation as rows [N*H*W, C],
+    w = the folded GEMM weight [Cout, k*k*C] with (kh, kw, c) columns (conv_weight_prep), output
+    rows [N*Ho*Wo, Cout] = epilogue(conv(x)) — the same products, in the same K order, as
+    gemm(im2col_nhwc(x), w) without the im2col matrix (im2im_retrieval.py:14-17, 29-36).
+    `x_planes`: split3(x), reused by the split-operand fp32 path when given. Returns (y, Ho, Wo)."""
+    _require_cuda(x, w, bias, residual)
+    if x.dtype != w.dtype:
+        raise TypeError(f"conv operands must share a dtype ({x.dtype} vs {w.dtype})")
+    if not conv_implicit_ok(x.dtype, C) or tuple(x.shape) != (N * H * W, C) or not x.is_contiguous():
+        raise ValueError(f"conv2d_nhwc: x must be contiguous [N*H*W, C] with C % {64 if x.dtype == torch.bfloat16 else 32} == 0")
+    Cout, Kw = w.shape
+    if Kw != k * k * C or not w.is_contiguous():
+        raise ValueError(f"conv2d_nhwc: w must be contiguous [Cout, {k * k * C}], got {tuple(w.shape)}")
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    M, K = N * Ho * Wo, k * k * C
+    out = torch.empty((M, Cout), device=x.device, dtype=x.dtype)
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Cout or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous fp32 vector of length Cout")
+    if residual is not None and (residual.dtype != out.dtype or tuple(residual.shape) != (M, Cout)):
+        raise ValueError("residual must match the output shape and dtype")
+    g = ConvGeomArgs(N=N, H=H, W=W, C=C, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Wo)
+    a = GemmArgs()
+    a.dtype = a.c_dtype = dtype_code(x.dtype)
+    a.M, a.N, a.K = M, Cout, K
+    a.A, a.lda, a.B, a.ldb = x.data_ptr(), C, w.data_ptr(), K
+    a.C, a.ldc = out.data_ptr(), Cout
+    a.alpha = 1.0
+    if bias is not None:
+        a.ep.bias = bias.data_ptr()
+    if residual is not None:
+        a.ep.residual, a.ep.ldr = residual.data_ptr(), _ld(residual)
+        a.ep.residual_first = int(bool(residual_first))
+    a.ep.act = int(act)
+    if x_planes is not None:
+        if x_planes.dtype != torch.bfloat16 or tuple(x_planes.shape) != (3, N * H * W, C) or not x_planes.is_contiguous():
+            raise ValueError("x_planes must be split3(x): contiguous bf16 [3, N*H*W, C]")
+        a.a_planes = x_planes.data_ptr()
+    a.conv = ctypes.addressof(g)
+    need = lib().mmfd_gemm_workspace_bytes(ctypes.byref(a))
+    if need < 0:
+        raise RuntimeError("mmfd_gemm_workspace_bytes failed: " + lib().mmfd_last_error_string().decode())
+    ws = torch.empty(max(need, 1), device=x.device, dtype=torch.uint8) if need > 0 else None
+    if ws is not None:
+        a.workspace, a.workspace_bytes = ws.data_ptr(), need
+    probe = _PROBE
+    rec = probe is not None and not torch.cuda.is_current_stream_capturing()
+    if rec:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _check(lib().mmfd_gemm(ctypes.byref(a), _stream()), "mmfd_gemm (conv)")
+    if rec:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        split = lib().mmfd_gemm_splits(ctypes.byref(a)) > 1
+        name = ("conv_x6f_kernel" if _x6(a) == 2 else
+                f"conv_mfma_kernel<{'__bf16' if x.dtype == torch.bfloat16 else 'float'}, "
+                f"{'__bf16' if x.dtype == torch.bfloat16 else 'float'}>") + (" (split-K)" if split else "")
+        probe.records.append((name, 2 * M * Cout * K, e0, e1))
     return out, Ho, Wo
 
 
