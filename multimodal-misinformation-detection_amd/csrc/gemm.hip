@@ -24,15 +24,20 @@ namespace {
 
 // CONV: implicit-GEMM convolution (ConvGeom): A is the NHWC activation and its fill gathers the
 // im2col rows per K-tile (ConvFill); TA = 0 only. The body is shared by gemm_mfma_kernel and
-// conv_mfma_kernel (two kernel names, so the plain GEMM's name in traces stays what it was)
-template <typename T, int TA, int TB, typename TC, bool CONV>
+// conv_mfma_kernel (two kernel names, so the plain GEMM's name in traces stays what it was).
+// BNT: the tile's N width — 128, or 64 for N <= 64 (the ResNet stem / layer1 convolutions: a 128-wide
+// tile spent half its MFMAs on zero columns); BNT = 64 takes K-contiguous B only (TB = 0)
+template <typename T, int TA, int TB, typename TC, bool CONV, int BNT = BN>
 __device__ __forceinline__ void
 gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
                int64_t K, float alpha, int tiles_per_split, const EpiArgs& e, const ConvGeom& cg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(BNT == BN || (BNT == 64 && TB == 0), "the 64-wide tile takes K-contiguous B only");
+  constexpr int BBYTES = BNT * ROWB, SBYTES = A_BYTES + BBYTES;  // B image, one stage
+  constexpr int WNS = BNT / 32;                     // 16-column subtiles per wave (2 wave columns)
   constexpr int APIECES = A_BYTES / 1024 / NWAVES;  // 4 pieces per wave
-  constexpr int BPIECES = B_BYTES / 1024 / NWAVES;  // 2 pieces per wave
+  constexpr int BPIECES = BBYTES / 1024 / NWAVES;   // 2 (1 for BNT = 64) pieces per wave
   constexpr int PIECES = APIECES + BPIECES;         // DMA instructions per wave per tile
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -42,24 +47,24 @@ gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   const int lin = blockIdx.y * gx + blockIdx.x;
   const int tile = xcd_remap(lin, gx * gy);
   const int tm = tile / gx, tn = tile % gx;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BNT;
 
   const int nkt_total = (int)((K + GT<T>::BK - 1) / GT<T>::BK);
   const int kt0 = blockIdx.z * tiles_per_split;
   const int nk = min(nkt_total, kt0 + tiles_per_split) - kt0;
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][WNS];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < WNS; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int64_t a_bytes = CONV ? cg.H * cg.W * cg.C * (M / (cg.Ho * cg.Wo)) * (int64_t)sizeof(T)
                                : (TA == 0 ? M : K) * lda * (int64_t)sizeof(T);
   const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, a_bytes);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(B, (TB == 0 ? N : K) * ldb * (int64_t)sizeof(T));
   std::conditional_t<CONV, ConvFill<T, APIECES>, Fill<T, TA, BM, APIECES>> fa;
-  Fill<T, TB, BN, BPIECES> fb;
+  Fill<T, TB, BNT, BPIECES> fb;
   if constexpr (CONV) fa.init(cg, m0, M, wave, lane);
   else fa.init(lda, m0, M, wave, lane);
   fb.init(ldb, n0, N, wave, lane);
@@ -67,7 +72,7 @@ gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   auto issue = [&](int t) {
     const int64_t k0 = (int64_t)(kt0 + t) * GT<T>::BK;
     const bool tail = k0 + GT<T>::BK > K;
-    char* st = smem + (t % NSTAGE) * STAGE_BYTES;
+    char* st = smem + (t % NSTAGE) * SBYTES;
     if constexpr (CONV) fa.issue(rsa, st, cg, k0, K, wave);
     else fa.issue(rsa, st, (uint32_t)(k0 * (TA == 0 ? 1 : lda) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
     fb.issue(rsb, st + A_BYTES, (uint32_t)(k0 * (TB == 0 ? 1 : ldb) * (int64_t)sizeof(T)), tail, k0, K, wave, lane);
@@ -83,19 +88,19 @@ gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + 2 < nk) issue(t + 2);
-    const char* la = smem + (t % NSTAGE) * STAGE_BYTES;
+    const char* la = smem + (t % NSTAGE) * SBYTES;
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kc = 0; kc < GT<T>::KCH; ++kc) {
-      uint4 xa[4], xb[4];
+      uint4 xa[4], xb[WNS];
 #pragma unroll
       for (int i = 0; i < 4; ++i) xa[i] = load_frag<T, TA, BM>(la, wm * 4 + i, kc, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xb[j] = load_frag<T, TB, BN>(lb, wn * 4 + j, kc, lane);
+      for (int j = 0; j < WNS; ++j) xb[j] = load_frag<T, TB, BNT>(lb, wn * WNS + j, kc, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], xa[i], xb[j]);
+        for (int j = 0; j < WNS; ++j) Mma<T>::run(acc[i][j], xa[i], xb[j]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -103,7 +108,7 @@ gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 
   // ---- epilogue: stage the 256x128 fp32 tile through LDS in four 64-row quarters (one wave row
   // each), then every thread handles 4 consecutive columns of a row (coalesced stores).
-  constexpr int LDC = BN + 4;
+  constexpr int LDC = BNT + 4;
   float* ct = reinterpret_cast<float*>(smem);
   const int g = lane >> 4, ci = lane & 15;
   const uint32_t seed = (!ws && e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
@@ -114,14 +119,14 @@ gemm_mfma_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WNS; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ct[(i * 16 + 4 * g + r) * LDC + wn * 64 + j * 16 + ci] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r) ct[(i * 16 + 4 * g + r) * LDC + wn * (BNT / 2) + j * 16 + ci] = acc[i][j][r];
     }
     __syncthreads();
-    // 64 rows x 16 groups of 8 columns; 2 groups per thread
-    for (int idx = tid; idx < 64 * (BN / 8); idx += NT) {
-      const int lr = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
+    // 64 rows x BNT/8 groups of 8 columns
+    for (int idx = tid; idx < 64 * (BNT / 8); idx += NT) {
+      const int lr = idx / (BNT / 8), c8 = (idx % (BNT / 8)) * 8;
       const int64_t row = m0 + qtr * 64 + lr;
       const int64_t col = n0 + c8;
       if (row >= M || col >= N) continue;
@@ -159,13 +164,21 @@ gemm_mfma_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, 
                  int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
   gemm_mfma_body<T, TA, TB, TC, false>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, ConvGeom{});
 }
+// the 256x64 tile for N <= 64 with K-contiguous B
+template <typename T, int TA, typename TC>
+__global__ void __launch_bounds__(NT, 1)
+gemm_mfma_n64_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                     TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N,
+                     int64_t K, float alpha, int tiles_per_split, EpiArgs e) {
+  gemm_mfma_body<T, TA, 0, TC, false, 64>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, ConvGeom{});
+}
 // implicit-GEMM convolution on the 256x128 kernel (mmfd_gemm_args.conv): A = the NHWC activation
-template <typename T, typename TC>
+template <typename T, typename TC, int BNT>
 __global__ void __launch_bounds__(NT, 1)
 conv_mfma_kernel(const T* __restrict__ X, const T* __restrict__ B, int64_t ldb, TC* __restrict__ C, int64_t ldc,
                  float* __restrict__ ws, int64_t M, int64_t N, int64_t K, float alpha, int tiles_per_split, EpiArgs e,
                  ConvGeom cg) {
-  gemm_mfma_body<T, 0, 0, TC, true>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, cg);
+  gemm_mfma_body<T, 0, 0, TC, true, BNT>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, cg);
 }
 
 template <typename TC>
@@ -241,6 +254,20 @@ __global__ void gemm_simple_kernel(const T* __restrict__ A, int64_t lda, int ta,
 template <typename T, int TA, int TB, typename TC>
 void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps,
                  hipStream_t s) {
+  if constexpr (TB == 0) {
+    if (a.N <= 64) {  // the 256x64 tile (no zero half-tile of B)
+      dim3 grid(1u, (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
+      constexpr int lds = NSTAGE * (A_BYTES + 64 * ROWB);
+      static bool attr64 = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mfma_n64_kernel<T, TA, TC>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+      }();
+      (void)attr64;
+      hipLaunchKernelGGL((gemm_mfma_n64_kernel<T, TA, TC>), grid, dim3(NT), lds, s, (const T*)a.A, a.lda,
+                         (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e);
+      return;
+    }
+  }
   dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mfma_kernel<T, TA, TB, TC>),
@@ -251,17 +278,24 @@ void launch_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
                      (const T*)a.A, a.lda, (const T*)a.B, a.ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K,
                      a.alpha, tps, e);
 }
+template <typename T, typename TC, int BNT>
+void launch_conv_mfma_t(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s,
+                        const ConvGeom& cg) {
+  dim3 grid((unsigned)((a.N + BNT - 1) / BNT), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
+  constexpr int lds = NSTAGE * (A_BYTES + BNT * ROWB);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_mfma_kernel<T, TC, BNT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((conv_mfma_kernel<T, TC, BNT>), grid, dim3(NT), lds, s, (const T*)a.A, (const T*)a.B, a.ldb,
+                     (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, cg);
+}
 template <typename T, typename TC>
 void launch_conv_mfma(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits, int tps, hipStream_t s,
                       const ConvGeom& cg) {
-  dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), (unsigned)splits);
-  static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_mfma_kernel<T, TC>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
-  }();
-  (void)attr;
-  hipLaunchKernelGGL((conv_mfma_kernel<T, TC>), grid, dim3(NT), LDS_BYTES, s, (const T*)a.A, (const T*)a.B, a.ldb,
-                     (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, cg);
+  if (a.N <= 64) launch_conv_mfma_t<T, TC, 64>(a, e, ws, splits, tps, s, cg);
+  else launch_conv_mfma_t<T, TC, BN>(a, e, ws, splits, tps, s, cg);
 }
 
 

@@ -411,6 +411,8 @@ def _kernel_name(a, split):
         else:
             base = (f"gemm256_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
                     f"{'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
+    elif a.N <= 64 and not a.trans_b:  # gemm.hip launch_mfma: the 256x64 tile
+        base = f"gemm_mfma_n64_kernel<{t[a.dtype]}, {a.trans_a}, {t[a.c_dtype]}>"
     else:
         base = f"gemm_mfma_kernel<{t[a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}>"
     return base + (" (split-K)" if split else "")
@@ -970,9 +972,9 @@ def conv2d_nhwc(x, N, H, W, C, w, k, stride, pad, bias=None, act=ACT_NONE, resid
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         split = lib().mmfd_gemm_splits(ctypes.byref(a)) > 1
+        tn = "__bf16" if x.dtype == torch.bfloat16 else "float"
         name = ("conv_x6f_kernel" if _x6(a) == 2 else
-                f"conv_mfma_kernel<{'__bf16' if x.dtype == torch.bfloat16 else 'float'}, "
-                f"{'__bf16' if x.dtype == torch.bfloat16 else 'float'}>") + (" (split-K)" if split else "")
+                f"conv_mfma_kernel<{tn}, {tn}, {64 if Cout <= 64 else 128}>") + (" (split-K)" if split else "")
         probe.records.append((name, 2 * M * Cout * K, e0, e1))
     return out, Ho, Wo
 

@@ -97,3 +97,24 @@ def test_conv_implicit_rejects_bad_geometry():
     xd = torch.randn(2 * 8 * 8, 64, device=DEV)
     with pytest.raises(ValueError):
         K.conv2d_nhwc(xd, 2, 8, 8, 64, torch.randn(64, 9 * 64 + 8, device=DEV), 3, 1, 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N", [64, 48, 16])
+@pytest.mark.parametrize("trans_a", [False, True])
+def test_gemm_narrow_tile(N, trans_a, dtype):
+    """tall GEMMs with N <= 64 and K-contiguous B run on the 256x64 tile (gemm_mfma_n64_kernel: the
+    ResNet stem and layer-1 convolutions, 1x1 and 3x3): against fp64, ragged M and K, with the
+    bias + ReLU epilogue and split-K"""
+    M, Kd = 4096 + 200, 152
+    g = torch.Generator().manual_seed(N + 3 * int(trans_a))
+    A = torch.randn((Kd, M) if trans_a else (M, Kd), generator=g)
+    B = torch.randn(N, Kd, generator=g) / Kd ** 0.5
+    b = torch.randn(N, generator=g)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    ref = F.relu((Ad.double().cpu().T if trans_a else Ad.double().cpu()) @ Bd.double().cpu().T + b.double())
+    for splits in (0, 3):
+        y = K.gemm(Ad, Bd, trans_a=trans_a, bias=b.to(DEV), act=K.ACT_RELU, splits=splits)
+        torch.cuda.synchronize()
+        err = (y.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= (1e-5 if dtype == torch.float32 else 8e-3), (splits, err)
