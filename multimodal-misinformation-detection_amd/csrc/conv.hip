@@ -58,32 +58,48 @@ __global__ void im2col_nhwc_kernel(int64_t N, int64_t H, int64_t W, int64_t C, i
   }
 }
 
-// stem im2col straight from the fp32 NCHW pixel tensor (C = 3): out[row][(kh*KW + kw)*C + c]. One
-// thread per (output row, kh): its KW*C outputs are contiguous (the KH threads of a row write one
-// contiguous K row), its loads are KW consecutive pixels of each channel row; 32-bit index math (the
-// host checks the sizes), the K padding columns written by the kh = KH-1 thread. (The first form —
-// one thread per output element with 64-bit divisions for every index — ran at ~0.9 TB/s.)
+// stem im2col straight from the fp32 NCHW pixel tensor (C = 3): out[row][(kh*KW + kw)*C + c].
+// Consecutive threads write consecutive output elements (coalesced: the output is the big side,
+// 1.95 GB at bs = 256 fp32); each block walks 16 rows at a time; the k -> (c, kh, kw) decomposition
+// comes from per-block LDS tables (pixel offset of the tap, kh, kw; kh = -1 for the K padding
+// columns), so an element costs three 32-bit divisions (row, pixel) and one gathered load (the
+// pixels are L2 hits: each is read by ~KH*KW/stride^2 windows). Round 1's form — one thread per
+// element with 64-bit divisions for every index — ran at ~0.9 TB/s (2.1 ms at bs = 256), a
+// thread-per-(row, kh) form with 21 scalar stores per thread 3x slower still.
+constexpr int kStemKmax = 512;
 template <typename T>
 __global__ void __launch_bounds__(256) im2col_nchw_kernel(uint32_t N, uint32_t C, uint32_t H, uint32_t W, uint32_t KH,
                                                           uint32_t KW, uint32_t stride, uint32_t pad, uint32_t Ho,
                                                           uint32_t Wo, uint32_t Kpad, const float* __restrict__ x,
                                                           T* __restrict__ out) {
-  const uint32_t total = N * Ho * Wo * KH;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
-    const uint32_t row = i / KH, kh = i - row * KH;
-    const uint32_t wo = row % Wo, t = row / Wo, ho = t % Ho, n = t / Ho;
-    const int hi = (int)(ho * stride + kh) - (int)pad;
-    const int wi0 = (int)(wo * stride) - (int)pad;
-    T* o = out + (size_t)row * Kpad + kh * KW * C;
-    const bool hin = hi >= 0 && hi < (int)H;
-    for (uint32_t kw = 0; kw < KW; ++kw) {
-      const int wi = wi0 + (int)kw;
-      const bool in = hin && wi >= 0 && wi < (int)W;
-      for (uint32_t c = 0; c < C; ++c)
-        o[kw * C + c] = from_f32<T>(in ? x[((size_t)(n * C + c) * H + (uint32_t)hi) * W + (uint32_t)wi] : 0.f);
+  __shared__ int tap_off[kStemKmax];
+  __shared__ short tap_kh[kStemKmax], tap_kw[kStemKmax];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t k = tid; k < Kpad; k += 256) {
+    if (k < KH * KW * C) {
+      const uint32_t c = k % C, kk = k / C, kw = kk % KW, kh = kk / KW;
+      tap_off[k] = (int)(c * H * W + kh * W + kw);
+      tap_kh[k] = (short)kh;
+      tap_kw[k] = (short)kw;
+    } else {
+      tap_off[k] = 0; tap_kh[k] = -1; tap_kw[k] = 0;
     }
-    if (kh == KH - 1)
-      for (uint32_t k = KH * KW * C; k < Kpad; ++k) out[(size_t)row * Kpad + k] = from_f32<T>(0.f);
+  }
+  __syncthreads();
+  constexpr uint32_t RB = 16;
+  const uint32_t rows = N * Ho * Wo;
+  for (uint32_t r0 = blockIdx.x * RB; r0 < rows; r0 += gridDim.x * RB) {
+    const uint32_t nel = min(RB, rows - r0) * Kpad;
+    for (uint32_t idx = tid; idx < nel; idx += 256) {
+      const uint32_t rl = idx / Kpad, k = idx - rl * Kpad, row = r0 + rl;
+      const uint32_t wo = row % Wo, t = row / Wo, ho = t % Ho, n = t / Ho;
+      const int kh = tap_kh[k];
+      const int hi = (int)(ho * stride) - (int)pad + kh, wi = (int)(wo * stride) - (int)pad + tap_kw[k];
+      float v = 0.f;
+      if (kh >= 0 && hi >= 0 && hi < (int)H && wi >= 0 && wi < (int)W)
+        v = x[(size_t)n * C * H * W + (size_t)(tap_off[k] + (int)(ho * stride - pad) * (int)W + (int)(wo * stride) - (int)pad)];
+      out[(size_t)row * Kpad + k] = from_f32<T>(v);
+    }
   }
 }
 
@@ -183,9 +199,9 @@ extern "C" int mmfd_im2col_nchw(int dtype, int64_t N, int64_t C, int64_t H, int6
                                 int pad, int64_t Ho, int64_t Wo, int64_t Kpad, const float* x, void* out,
                                 mmfd_stream_t stream) {
   MMFD_CHECK_ARG(Kpad >= (int64_t)KH * KW * C, "im2col_nchw: Kpad too small");
-  MMFD_CHECK_ARG(N * C * H * W < (1ll << 32) && N * Ho * Wo * KH < (1ll << 32) && KH > 0 && KW > 0 && stride > 0,
-                 "im2col_nchw: sizes past the 32-bit index range");
-  const int64_t n = N * Ho * Wo * KH;
+  MMFD_CHECK_ARG(C * H * W < (1ll << 31) && N * Ho * Wo < (1ll << 31) && Kpad <= kStemKmax && KH > 0 && KW > 0 &&
+                 stride > 0, "im2col_nchw: sizes past the kernel's index range (Kpad <= %d)", kStemKmax);
+  const int64_t n = (N * Ho * Wo + 15) / 16 * 256;  // 16 rows per block-iteration
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMFD_BF16)
