@@ -19,6 +19,11 @@ the point. Variants (template V): 0 = MFMAs only (barriers kept), 1 = MFMAs + fr
 2 = full loop with reads and DMA spread through the MFMAs, 3 = full loop with each part's reads and
 DMA issued as one burst before its MFMAs, 4 = V2 followed by a register epilogue (16-B nontemporal
 stores of 256-B row segments, no LDS) into the tile of a [65536][3072] bf16 output.
+Round 6 (what a DMA piece costs; profiles/r06_g4loop_mb_dma_*.log): 5 / 6 = V2 with each wave's DMA
+slot shifted by 2 / 1 MFMAs per wave (the four waves never issue a piece in the same MFMA gap),
+7 = V5 with the fragment reads shifted too, 8 = V2 without the per-piece m0 writes, 9 = V2 with
+plain 16-B buffer loads into a VGPR quad instead of LDS-DMA, 10 = V2 with 4-B LDS-DMA pieces
+(timing only: 8-10 place data wrongly).
   python3 tools/mb/gen_g4loop.py && hipcc -O3 --offload-arch=gfx950 tools/mb/g4loop.hip -o tools/mb/g4loop
 """
 import os
