@@ -426,6 +426,11 @@ int mmfd_adamw(int n_tensors, const mmfd_adamw_tensor* table, int64_t max_numel,
 /* ------------------------------------------------------------------------------------------- */
 /* out(dtype_out) = in(dtype_in) * scale (+ add) — casts / scaled copies / grad accumulation. */
 int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream);
+/* out[c][r] = in[r][c] (fp32 or bf16, row-major with leading dims ldi >= cols, ldo >= rows; no
+   aliasing): the K-contiguous copy of an nn.Linear weight that lets its data-gradient GEMM run in
+   the forward operand layout (the four-wave GEMM), refreshed once per step */
+int mmfd_transpose(int dtype, int64_t rows, int64_t cols, const void* in, int64_t ldi, void* out, int64_t ldo,
+                   mmfd_stream_t stream);
 /* dst[0 .. bytes) = 0 on the stream, by a kernel (graph-capture safe); the scatter-add targets of
    the embedding backward */
 int mmfd_zero(void* dst, int64_t bytes, mmfd_stream_t stream);

@@ -164,6 +164,16 @@ class StepCtx:
             self._w[key] = t
         return t
 
+    def wT(self, name):
+        """the K-contiguous copy W^T [in, out] of weight `name.weight` in compute dtype (mmfd_transpose
+        of the shadow, made once per step: the data-gradient GEMM dY W then runs in the forward
+        operand layout, on the four-wave kernel)"""
+        key = name + "^T"
+        t = self._w.get(key)
+        if t is None:
+            t = self._w[key] = K.transpose(self.w(name))
+        return t
+
     def b(self, name):
         return self.P.get(name + ".bias")
 
@@ -373,8 +383,35 @@ def linear_packed(ctx: StepCtx, x2d, names, xp=None):
     return K.gemm(x2d, W, bias=b, a_planes=xp, b_planes=ctx.wplanes(W) if xp is not None else None)
 
 
+# A/B switch (same-box bench comparisons): 0 = never, 2 = also past the four-wave kernel's K limit
+# (those products then run on gemm256_kernel in the forward layout)
+DX_TRANSPOSED = os.environ.get("MMFD_DX_TRANSPOSED", "1")
+
+
+def _dx_forward_layout(ctx, dy2d, name_or_W, out, beta, act, residual, drop_site):
+    """whether dY W runs better as dY (W^T)^T with the transposed weight copy: bf16 products the
+    four-wave GEMM takes in the forward layout (K = out features <= its K limit, full 256x256
+    tiles; a plain, + residual or GELU-backward epilogue) — the FFN2 and attention-output data
+    gradients"""
+    if DX_TRANSPOSED == "0" or ctx.dt != torch.bfloat16 or not isinstance(name_or_W, str) or out is not None:
+        return False
+    if beta != 0.0:
+        return False
+    if drop_site is not None or act not in (K.ACT_NONE, K.ACT_GELU_BWD) or (residual is not None and act != K.ACT_NONE):
+        return False
+    mode, kmax = K.g4_mode()
+    if mode == "off":
+        return False
+    nout, nin = ctx.P[name_or_W + ".weight"].shape
+    if DX_TRANSPOSED == "2":
+        kmax = 1 << 30
+    return dy2d.shape[0] % 256 == 0 and nin % 256 == 0 and nout % 64 == 0 and 64 <= nout <= kmax
+
+
 def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
               residual=None, dyp=None, out_planes=None, write_out=True):
+    if _dx_forward_layout(ctx, dy2d, name_or_W, out, beta, act, residual, drop_site):
+        return K.gemm(dy2d, ctx.wT(name_or_W), act=act, aux=aux, residual=residual)
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W
     return K.gemm(dy2d, W, trans_b=True, out=out, beta=beta if out is not None else 0.0, act=act, aux=aux,
                   residual=residual, a_planes=dyp, b_planes=ctx.wplanes(W) if dyp is not None else None,

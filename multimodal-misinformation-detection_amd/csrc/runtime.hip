@@ -87,6 +87,44 @@ __global__ void act_bwd_kernel(int64_t n, int64_t width, const T* __restrict__ d
 
 }  // namespace
 
+// out[c][r] = in[r][c] for 2- or 4-byte elements: 64x64 tiles through LDS (one padding column:
+// conflict-free column reads), 256 threads, every global access a coalesced row segment
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_kernel(int64_t rows, int64_t cols, const T* __restrict__ in,
+                                                        int64_t ldi, T* __restrict__ out, int64_t ldo) {
+  __shared__ T tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t r = r0 + ty + 4 * k, c = c0 + tx;
+    if (r < rows && c < cols) tile[ty + 4 * k][tx] = in[r * ldi + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t c = c0 + ty + 4 * k, r = r0 + tx;
+    if (c < cols && r < rows) out[c * ldo + r] = tile[tx][ty + 4 * k];
+  }
+}
+
+extern "C" int mmfd_transpose(int dtype, int64_t rows, int64_t cols, const void* in, int64_t ldi, void* out, int64_t ldo,
+                              mmfd_stream_t stream) {
+  MMFD_CHECK_ARG(dtype == MMFD_F32 || dtype == MMFD_BF16, "mmfd_transpose: dtype %d", dtype);
+  MMFD_CHECK_ARG(rows >= 0 && cols >= 0 && ldi >= cols && ldo >= rows, "mmfd_transpose: bad shape / leading dims");
+  if (rows == 0 || cols == 0) return 0;
+  MMFD_CHECK_ARG(in && out && in != out, "mmfd_transpose: null or aliased pointers");
+  MMFD_CHECK_ARG((rows + 63) / 64 < 65536, "mmfd_transpose: too many rows");
+  const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMFD_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, s, rows, cols, (const bf16*)in, ldi, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, s, rows, cols, (const float*)in, ldi, (float*)out, ldo);
+  MMFD_CHECK_LAUNCH("transpose");
+  return 0;
+}
+
 extern "C" int mmfd_cast(int dtype_in, int dtype_out, int64_t n, const void* in, void* out, mmfd_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;

@@ -140,6 +140,7 @@ SIGNATURES = {
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_gemm_runs_split": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_set_g4_mode": (_I, [_I]),
+    "mmfd_transpose": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _I64, _VP]),
     "mmfd_set_g4_kmax": (_I64, [_I64]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
     "mmfd_layernorm_fwd_split": (_I, [_I64, _I64, _VP, _I64, _VP, _VP, _F, _VP, _I64, _VP, _VP, _VP, _VP]),
@@ -499,6 +500,8 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
         return 2 if dropout_p > 0 else 1
     if act == ACT_GELU and residual is None and dropout_p <= 0 and g4 == "gelu":
         return 3
+    if act == ACT_GELU_BWD and aux is not None and residual is None and dropout_p <= 0:
+        return 4
     return None
 
 
@@ -782,6 +785,21 @@ def cast(x, dtype, out=None):
         raise ValueError("cast: out must be a contiguous tensor of the target dtype and size")
     if x.numel():
         _ops().cast(x if x.is_contiguous() else x.contiguous(), out)
+    return out
+
+
+def transpose(x, out=None):
+    """out = x^T as a contiguous [cols, rows] tensor (fp32 / bf16, mmfd_transpose)"""
+    _require_cuda(x)
+    if x.dim() != 2:
+        raise ValueError("transpose takes a 2-D tensor")
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty((cols, rows), device=x.device, dtype=x.dtype)
+    if out.dtype != x.dtype or tuple(out.shape) != (cols, rows):
+        raise ValueError("transpose: out must be [cols, rows] of the input dtype")
+    _check(lib().mmfd_transpose(dtype_code(x.dtype), rows, cols, _ptr(x), _ld(x), _ptr(out), _ld(out), _stream()),
+           "mmfd_transpose")
     return out
 
 

@@ -115,6 +115,39 @@ def test_gemm_bf16_g4_forward(shape, with_bias, g4_restore):
     assert diff <= ulp, (diff, ulp)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(768, 3072), (3072, 768), (77, 130), (1, 64), (300, 1)])
+def test_transpose_exact(shape, dtype):
+    """mmfd_transpose (the per-step K-contiguous weight copy): exact, odd shapes and a strided view"""
+    x = _rand(*shape, dtype=dtype, seed=shape[0] + shape[1]).to(DEV)
+    assert torch.equal(K.transpose(x), x.t().contiguous())
+    wide = _rand(shape[0], shape[1] + 8, dtype=dtype, seed=5).to(DEV)
+    v = wide[:, 8:]
+    assert torch.equal(K.transpose(v), v.t().contiguous())
+
+
+@pytest.mark.parametrize("act", ["none", "gelu_bwd"])
+@pytest.mark.parametrize("shape", [(512, 3072, 768), (768, 768, 768), (256, 256, 64)])
+def test_gemm_bf16_dx_forward_layout_matches_trans_b(shape, act, g4_restore):
+    """the bf16 data-gradient GEMM dY W run as dY (W^T)^T on the four-wave kernel (blocks.linear_dx
+    with the transposed weight copy; EPI 4 = x GELU'(pre-activation)) gives the same bits as the
+    product with W as the MN-contiguous operand on gemm256_kernel"""
+    M, N, Kd = shape  # dY [M, Kd] (out features), W [Kd, N] (nn.Linear [out, in])
+    dy = _rand(M, Kd, dtype=torch.bfloat16, seed=M + 1).to(DEV)
+    W = _rand(Kd, N, dtype=torch.bfloat16, seed=N + 2).to(DEV)
+    kw = {}
+    if act == "gelu_bwd":
+        kw = dict(act=K.ACT_GELU_BWD, aux=_rand(M, N, dtype=torch.bfloat16, seed=3).to(DEV))
+    K.set_g4_mode("on")
+    g4 = K.gemm(dy, K.transpose(W), **kw)
+    ref = K.gemm(dy, W, trans_b=True, **kw)
+    K.set_g4_mode("off")
+    g8 = K.gemm(dy, K.transpose(W), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(g4, g8), (g4.float() - g8.float()).abs().max().item()
+    assert torch.equal(g4, ref), (g4.float() - ref.float()).abs().max().item()
+
+
 @pytest.mark.parametrize("Kd", [64, 768])
 @pytest.mark.parametrize("mode", ["bias", "gelu_aux", "dropout_residual"])
 def test_gemm_bf16_g4_strided_views_match_g8(Kd, mode, g4_restore):
