@@ -2435,12 +2435,15 @@ void launch_fwd_v2_hpb(const AttnP& p, hipStream_t s) {
                      dim3(V2_THREADS), lds, s, p);
 }
 
-// the fixed v2 mode for these arguments (see V2_RESCALE_TH): 1 plain, 2 hashed dropout + key bias,
-// 0 anything else (relative bias, keep-bitmask, dropout without a key bias, ...)
+// the fixed v2 mode for these arguments (see V2_RESCALE_TH): 1 plain, 2 hashed dropout with or
+// without a key bias (the per-key bias vector is staged either way: 0 for real keys when there is
+// none, -inf for the padding — round 6: the fusion head's dropout-only attention had run the
+// generic mode at ~50 VALU instructions per MFMA), 0 anything else (relative bias, keep-bitmask,
+// a key bias without dropout)
 inline int v2_mode(const AttnP& p) {
   if (p.rel_bias || g_v2_generic) return 0;
   if (p.p == 0.f && !p.key_bias) return 1;
-  if (p.p > 0.f && p.key_bias && !p.dm) return 2;
+  if (p.p > 0.f && !p.dm) return 2;
   return 0;
 }
 

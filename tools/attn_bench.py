@@ -14,8 +14,7 @@ import mmfd  # noqa: E402
 from mmfd import kernels as K  # noqa: E402
 
 
-def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False, bitmask=False):
-    B, H, D = 512, 12, 64
+def case(name, L, masked, p, iters, dtype=torch.bfloat16, planes=False, bitmask=False, B=512, H=12, D=64):
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(0)
     qkv = torch.randn(B, L, 3 * H * D, generator=g).to(dev, dtype)
@@ -86,3 +85,5 @@ if __name__ == "__main__":
                 case(f"{dt} bert L=128 mask p={a.bert_p} bitmask", 128, True, a.bert_p, a.iters, t, a.planes, True)
         if a.only in ("", "vit"):
             case(f"{dt} vit  L=197          ", 197, False, 0.0, a.iters, t, a.planes)
+        if a.only in ("", "head"):  # the fusion head: E = 256, 8 heads of D = 32, dropout, no key mask
+            case(f"{dt} head L=128 D=32 p=0.1  ", 128, False, 0.1, a.iters, t, a.planes, B=256, H=8, D=32)
