@@ -62,15 +62,17 @@ def _worker(rank, world, port, bucket_mb, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [64.0, 0.001])  # one bucket / many small buckets
-def test_grad_allreduce_gloo_world2(bucket_mb):
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world,bucket_mb", [(2, 64.0), (2, 0.001), (4, 0.001), (8, 0.001)])
+def test_grad_allreduce_gloo_world2(world, bucket_mb):
+    """one bucket / many small buckets; world 4 and 8 rehearse the node layout bench.py --gpus N
+    launches (gloo on the CPU: the 8-GPU run itself is the driver's)"""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = dict(q.get(timeout=240) for _ in range(world))
     res = {k: [torch.from_numpy(a) if a is not None else None for a in v] for k, v in res.items()}
     for p in procs:
         p.join(timeout=60)
@@ -80,7 +82,7 @@ def test_grad_allreduce_gloo_world2(bucket_mb):
         want = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * r + i)) for r in range(world)) / world
         for r in range(world):
             torch.testing.assert_close(res[r][i], want, rtol=1e-6, atol=1e-6)
-    assert res[0][5] is None and res[1][5] is None
+    assert all(res[r][5] is None for r in range(world))
     m = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Linear(7, 300))
     for i, (n, p) in enumerate(m.named_parameters()):
         want = sum(torch.randn(p.shape, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
