@@ -998,6 +998,13 @@ def train_leg(args, dev, world, rank, precision):
                              "achieved = 2MNK per launch / launch time")
         roof["bf16_mfma_view"] = {"achieved": round(6 * achieved, 1), "peak": PEAK_TFLOPS["bf16"],
                                   "note": "the same launches as executed bf16 MFMA FLOPs (6 x 2MNK) over the bf16 peak"}
+    # context, not the ceiling the frac is taken against: the bf16 MFMA rate this chip holds with no
+    # memory traffic at all (tools/mb/gen_g4loop.py V0, MFMAs only on pseudo-random operands,
+    # profiles/r06_g4loop_mb_dma_forms.log: 1,790-2,030 TFLOP/s of 2,516.6 = 0.71-0.81, the clock
+    # under MFMA load on random data), and what one 1-KB LDS-DMA / vector-memory instruction costs
+    # its wave among MFMAs (V2 / V8 / V9: ~45 cycles, not contention between waves, V5-V7)
+    roof["mfma_only_rate_note"] = ("bf16 MFMA-only loop on random operands: 0.71-0.81 of the dense peak "
+                                   "(power-limited clock; profiles/r06_g4loop_mb_dma_forms.log V0)")
     return {"pairs": pairs, "ms": ms, "loss": round(loss_val, 4), "loss_exact": loss_val, "gemm_ms": round(gemm_ms, 2), "gemm_kinds": kinds,
             "first_loss": None if first_loss is None else [round(v, 6) for v in first_loss.double().cpu().tolist()],
             "dp_check": dp_check,
