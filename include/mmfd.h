@@ -37,7 +37,9 @@ enum {
   MMFD_ACT_GELU_BWD = 3,  /* out *= gelu'(aux)  (aux = saved pre-activation) */
   MMFD_ACT_RELU_BWD = 4,  /* out *= (aux > 0)   */
   MMFD_ACT_TANH = 5,      /* tanh (HF BertPooler, the cross-encoder's [CLS] pooler), forward only */
-  MMFD_ACT_SIGMOID = 6    /* 1 / (1 + exp(-x)) (CrossEncoder's default score activation) */
+  MMFD_ACT_SIGMOID = 6,   /* 1 / (1 + exp(-x)) (CrossEncoder's default score activation) */
+  MMFD_ACT_GELU_D = 7,    /* GELU as MMFD_ACT_GELU, but aux <- gelu'(pre-activation) (training forward) */
+  MMFD_ACT_MUL_AUX = 8    /* out *= aux  (aux = a saved derivative: the MMFD_ACT_GELU_D backward) */
 };
 enum { MMFD_OK = 0, MMFD_ERR_INVALID = 1000, MMFD_ERR_UNSUPPORTED = 1001 };
 

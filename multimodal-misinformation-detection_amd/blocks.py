@@ -347,12 +347,23 @@ def as2d(x):
 # -------------------------------------------------------------------------------------------------
 # linear
 # -------------------------------------------------------------------------------------------------
+# the training forward's GELU keeps gelu'(pre-activation) instead of the pre-activation
+# (MMFD_ACT_GELU_D; one erf per element instead of one in the forward and one in the backward);
+# MMFD_GELU_DERIV=0 keeps the pre-activation (A/B switch)
+GELU_DERIV = os.environ.get("MMFD_GELU_DERIV", "1") != "0"
+
+
 def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=None, drop_site=None,
            out_dtype=None, xp=None, out_planes=None, write_out=True):
+    """(y, aux): with keep_aux, aux is what the activation's backward reads — the pre-activation,
+    or for GELU under GELU_DERIV its derivative (tagged _mmfd_gelu_d; linear_dx then multiplies)"""
     W = ctx.w(name)
     aux = None
     if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
         aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
+        if act == K.ACT_GELU and GELU_DERIV:
+            act = K.ACT_GELU_D
+            aux._mmfd_gelu_d = True
     y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,
                a_planes=xp, b_planes=ctx.wplanes(W) if xp is not None else None, out_planes=out_planes,
                write_out=write_out, **(ctx.drop(drop_site) if drop_site else {}))
@@ -397,7 +408,7 @@ def _dx_forward_layout(ctx, dy2d, name_or_W, out, beta, act, residual, drop_site
         return False
     if beta != 0.0:
         return False
-    if drop_site is not None or act not in (K.ACT_NONE, K.ACT_GELU_BWD) or (residual is not None and act != K.ACT_NONE):
+    if drop_site is not None or act not in (K.ACT_NONE, K.ACT_GELU_BWD, K.ACT_MUL_AUX) or (residual is not None and act != K.ACT_NONE):
         return False
     mode, kmax = K.g4_mode()
     if mode == "off":
@@ -410,6 +421,8 @@ def _dx_forward_layout(ctx, dy2d, name_or_W, out, beta, act, residual, drop_site
 
 def linear_dx(ctx: StepCtx, dy2d, name_or_W, *, out=None, beta=0.0, act=K.ACT_NONE, aux=None, drop_site=None,
               residual=None, dyp=None, out_planes=None, write_out=True):
+    if act == K.ACT_GELU_BWD and getattr(aux, "_mmfd_gelu_d", False):
+        act = K.ACT_MUL_AUX  # aux already holds gelu'(pre-activation)
     if _dx_forward_layout(ctx, dy2d, name_or_W, out, beta, act, residual, drop_site):
         return K.gemm(dy2d, ctx.wT(name_or_W), act=act, aux=aux, residual=residual)
     W = ctx.w(name_or_W) if isinstance(name_or_W, str) else name_or_W

@@ -84,6 +84,16 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
+// GELU and its derivative from one erf evaluation (MMFD_ACT_GELU_D): the operations of gelu_f and
+// gelu_grad_f, so both values are bit-identical to theirs — the backward's x gelu'(pre) becomes a
+// multiply by the saved derivative (MMFD_ACT_MUL_AUX) with the same fp32 result
+__device__ __forceinline__ float gelu_and_grad_f(float x, float& d) {
+  float e;
+  const float r = erf_fast(x * 0.70710678118654752f, e);
+  d = fmaf(x * 0.39894228040143268f, e, 0.5f * (1.0f + r));
+  return 0.5f * x * (1.0f + r);
+}
+
 // forward-only epilogue activations past ReLU (MMFD_ACT_TANH / MMFD_ACT_SIGMOID)
 __device__ __forceinline__ float act_tail_f(int act, float z) {
   return act == MMFD_ACT_TANH ? tanhf(z) : 1.0f / (1.0f + expf(-z));

@@ -315,7 +315,7 @@ void launch_g8(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits,
     return mmfd_gemmx::launch_g8_f32out<T, TA, TB, false>(a, e, ws, splits, tps, rs_out, rs_mode, s, a.A, a.lda, a.B,
                                                           a.ldb, none);
   } else {
-    const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD;
+    const bool bwd_act = e.act == MMFD_ACT_GELU_BWD || e.act == MMFD_ACT_RELU_BWD || e.act == MMFD_ACT_MUL_AUX;
     const int streams = (e.residual ? 1 : 0) + (bwd_act ? 1 : 0) + (e.beta != 0.f ? 1 : 0);
     if (streams == 1 && !ws && e.vec)
       return launch_g8_v<T, TA, TB, TC, true, false>(a, e, ws, splits, tps, rs_out, rs_mode, s, a.A, a.lda, a.B, a.ldb, none);
@@ -598,8 +598,9 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
                  "mmfd_gemm: out_planes need N %% 8 == 0 and 16-B alignment");
   MMFD_CHECK_ARG(a.ldc >= a.N, "mmfd_gemm: ldc %lld < N %lld", (long long)a.ldc, (long long)a.N);
   const int act = a.ep.act;
-  MMFD_CHECK_ARG(act >= 0 && act <= MMFD_ACT_SIGMOID, "mmfd_gemm: bad act %d", act);
-  MMFD_CHECK_ARG(!(act == MMFD_ACT_GELU_BWD || act == MMFD_ACT_RELU_BWD) || a.ep.aux != nullptr,
+  MMFD_CHECK_ARG(act >= 0 && act <= MMFD_ACT_MUL_AUX, "mmfd_gemm: bad act %d", act);
+  MMFD_CHECK_ARG(!(act == MMFD_ACT_GELU_BWD || act == MMFD_ACT_RELU_BWD || act == MMFD_ACT_MUL_AUX) ||
+                     a.ep.aux != nullptr,
                  "mmfd_gemm: backward act needs aux");
   MMFD_CHECK_ARG(a.ep.dropout_p <= 0.f || a.ep.seed != nullptr, "mmfd_gemm: dropout needs seed");
   MMFD_CHECK_ARG(a.ep.dropout_p < 1.f, "mmfd_gemm: dropout p must be < 1");

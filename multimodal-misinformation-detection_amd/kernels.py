@@ -29,6 +29,8 @@ F32, BF16, F16 = 0, 1, 2
 ABI_VERSION = 3  # include/mmfd.h MMFD_ABI_VERSION: the layout of the argument structs below
 COS_PAIR, COS_NORMALIZED, COS_ROUND_F16 = 0, 1, 4
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_BWD, ACT_RELU_BWD, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
+# GELU whose aux keeps gelu'(pre-activation), and its backward (out *= aux): the training FFNs
+ACT_GELU_D, ACT_MUL_AUX = 7, 8
 
 
 class NativeLibraryError(RuntimeError):
@@ -404,7 +406,7 @@ def _kernel_name(a, split):
     narrow = a.M >= 4096 and (a.N <= 128 or a.K < 64)  # gemm.hip use_g8
     g8 = not narrow and (a.dtype == BF16 or a.c_dtype == F32)
     if g8:  # 256x256 kernel; PRE = one prefetched bf16 epilogue operand stream; X6 = split operands
-        streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD)) + int(a.beta != 0.0)
+        streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD, ACT_MUL_AUX)) + int(a.beta != 0.0)
         pre = a.c_dtype == BF16 and streams == 1 and not split
         x6 = _x6(a)
         if x6 == 2:
@@ -502,6 +504,10 @@ def _g4_mode(A, B, out, trans_a, trans_b, residual, act, beta, splits, alpha, re
         return 3
     if act == ACT_GELU_BWD and aux is not None and residual is None and dropout_p <= 0:
         return 4
+    if act == ACT_GELU_D and residual is None and dropout_p <= 0 and g4 == "gelu":
+        return 5
+    if act == ACT_MUL_AUX and aux is not None and residual is None and dropout_p <= 0:
+        return 6
     return None
 
 

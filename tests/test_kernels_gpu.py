@@ -126,7 +126,7 @@ def test_transpose_exact(shape, dtype):
     assert torch.equal(K.transpose(v), v.t().contiguous())
 
 
-@pytest.mark.parametrize("act", ["none", "gelu_bwd"])
+@pytest.mark.parametrize("act", ["none", "gelu_bwd", "mul_aux"])
 @pytest.mark.parametrize("shape", [(512, 3072, 768), (768, 768, 768), (256, 256, 64)])
 def test_gemm_bf16_dx_forward_layout_matches_trans_b(shape, act, g4_restore):
     """the bf16 data-gradient GEMM dY W run as dY (W^T)^T on the four-wave kernel (blocks.linear_dx
@@ -138,6 +138,8 @@ def test_gemm_bf16_dx_forward_layout_matches_trans_b(shape, act, g4_restore):
     kw = {}
     if act == "gelu_bwd":
         kw = dict(act=K.ACT_GELU_BWD, aux=_rand(M, N, dtype=torch.bfloat16, seed=3).to(DEV))
+    elif act == "mul_aux":  # EPI 6: x the saved GELU derivative
+        kw = dict(act=K.ACT_MUL_AUX, aux=_rand(M, N, dtype=torch.bfloat16, seed=3).to(DEV))
     K.set_g4_mode("on")
     g4 = K.gemm(dy, K.transpose(W), **kw)
     ref = K.gemm(dy, W, trans_b=True, **kw)
@@ -189,7 +191,7 @@ def test_gemm_bf16_g4_strided_views_match_g8(Kd, mode, g4_restore):
         assert err <= 8e-3, err
 
 
-@pytest.mark.parametrize("mode", ["gelu_aux", "residual", "dropout_residual"])
+@pytest.mark.parametrize("mode", ["gelu_aux", "gelu_deriv", "residual", "dropout_residual"])
 def test_gemm_bf16_g4_epilogues_match_g8(mode, g4_restore):
     """the four-wave kernel's fused epilogues of the encoder forward Linears (FFN1: bias + GELU with
     the pre-activation to aux; attention output / FFN2: bias [+ hashed dropout] + residual) are
@@ -206,6 +208,8 @@ def test_gemm_bf16_g4_epilogues_match_g8(mode, g4_restore):
         aux = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
         if mode == "gelu_aux":
             out = K.gemm(A, B, bias=bias, act=K.ACT_GELU, aux=aux)
+        elif mode == "gelu_deriv":  # EPI 5: GELU with its derivative to aux
+            out = K.gemm(A, B, bias=bias, act=K.ACT_GELU_D, aux=aux)
         elif mode == "residual":
             out = K.gemm(A, B, bias=bias, residual=res)
         else:
@@ -217,10 +221,64 @@ def test_gemm_bf16_g4_epilogues_match_g8(mode, g4_restore):
     ref = A.double().cpu() @ B.double().cpu().T + bias.double().cpu()
     if mode == "residual":
         ref = ref + res.double().cpu()
+    if mode == "gelu_deriv":
+        t = ref.clone().requires_grad_(True)
+        torch.nn.functional.gelu(t).backward(torch.ones_like(t))
+        assert (outs["1"][1].double().cpu() - t.grad).abs().max().item() <= 1.2 * 2.0 ** -7
+        ref = torch.nn.functional.gelu(ref)
     if mode != "dropout_residual":
         got = outs["1"][1] if mode == "gelu_aux" else outs["1"][0]
         err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 8e-3, err
+
+
+# (M, N, K) reaching each kernel family: the 256x128 MFMA kernel (ragged), the split-operand x6f
+# kernel (fp32) / 256x256 kernels (bf16), a split-K product (long K, small output)
+@pytest.mark.parametrize("shape", [(300, 256, 128), (1024, 768, 768), (256, 192, 8192)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_gelu_deriv_pair(shape, dtype):
+    """MMFD_ACT_GELU_D / MMFD_ACT_MUL_AUX (the training FFN's forward GELU saving gelu'(z), and the
+    backward multiplying by it) against the pre-activation pair ACT_GELU / ACT_GELU_BWD: the forward
+    output is bit-identical in both precisions; in fp32 the saved derivative is gelu_grad_f of the
+    same fp32 z, so the backward product is bit-identical too (with caller-supplied split planes as
+    well); in bf16 both backward forms are within 1 bf16 ulp-scale of the fp64 reference"""
+    M, N, Kd = shape
+    x = _rand(M, Kd, dtype=dtype, seed=M + 71).to(DEV)
+    w = _rand(N, Kd, dtype=dtype, seed=N + 72, scale=0.1).to(DEV)
+    b = _rand(N, seed=73).to(DEV)
+    dy = _rand(M, Kd, dtype=dtype, seed=74).to(DEV)
+    w2 = _rand(Kd, N, dtype=dtype, seed=75, scale=0.1).to(DEV)  # stored [K][N]: trans_b
+    d = torch.empty(M, N, device=DEV, dtype=dtype)
+    pre = torch.empty(M, N, device=DEV, dtype=dtype)
+    y_d = K.gemm(x, w, bias=b, act=K.ACT_GELU_D, aux=d)
+    y_g = K.gemm(x, w, bias=b, act=K.ACT_GELU, aux=pre)
+    torch.cuda.synchronize()
+    assert torch.equal(y_d, y_g), (y_d.float() - y_g.float()).abs().max().item()
+    t = pre.double().cpu().requires_grad_(True)
+    torch.nn.functional.gelu(t).backward(torch.ones_like(t))
+    tol = 1e-6 if dtype == torch.float32 else 1.2 * 2.0 ** -7
+    assert (d.double().cpu() - t.grad).abs().max().item() <= tol * 1.2
+    # the backward's dY W2 (blocks.linear_dx layout: the weight MN-contiguous)
+    g_mul = K.gemm(dy, w2, trans_b=True, act=K.ACT_MUL_AUX, aux=d)
+    g_pre = K.gemm(dy, w2, trans_b=True, act=K.ACT_GELU_BWD, aux=pre)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert torch.equal(g_mul, g_pre), (g_mul - g_pre).abs().max().item()
+        if K.split_eligible(dy):
+            g_pl = K.gemm(dy, w2, trans_b=True, act=K.ACT_MUL_AUX, aux=d, a_planes=K.split3(dy),
+                          b_planes=K.split3(w2))
+            torch.cuda.synchronize()
+            assert torch.equal(g_pl, g_pre)
+    ref = (dy.double().cpu() @ w2.double().cpu()) * t.grad
+    scale = ref.abs().max().item()
+    for g in (g_mul, g_pre):
+        err = (g.double().cpu() - ref).abs().max().item() / scale
+        assert err <= (1e-5 if dtype == torch.float32 else 1.6e-2), err
+
+
+def test_gemm_mul_aux_needs_aux():
+    with pytest.raises((RuntimeError, ValueError)):
+        K.gemm(torch.randn(64, 64, device=DEV), torch.randn(64, 64, device=DEV), act=K.ACT_MUL_AUX)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

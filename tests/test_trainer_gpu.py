@@ -13,8 +13,13 @@ from tests.smoke_impl import TINY, build_pair, compare_step, tiny_batch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("gelu_deriv", [True, False])
 @pytest.mark.parametrize("dropout", [0.0, 0.1])
-def test_train_step_fp32_matches_oracle(dropout):
+def test_train_step_fp32_matches_oracle(dropout, gelu_deriv, monkeypatch):
+    """(gelu_deriv: the FFN forward saves gelu'(pre-activation) — MMFD_ACT_GELU_D — or the
+    pre-activation, blocks.GELU_DERIV)"""
+    from mmfd import blocks as Bk
+    monkeypatch.setattr(Bk, "GELU_DERIV", gelu_deriv)
     tr, ref = build_pair("fp32", dropout=dropout)
     for s in (1, 2):
         compare_step(tr, ref, tiny_batch(3, seed=s), loss_tol=1e-3, grad_rtol=2e-3)
@@ -26,7 +31,10 @@ def test_train_step_fp32_wider_matches_oracle():
     compare_step(tr, ref, tiny_batch(2, cfg=cfg, seed=3), loss_tol=1e-3, grad_rtol=2e-3)
 
 
-def test_train_step_bf16_close_to_oracle():
+@pytest.mark.parametrize("gelu_deriv", [True, False])
+def test_train_step_bf16_close_to_oracle(gelu_deriv, monkeypatch):
+    from mmfd import blocks as Bk
+    monkeypatch.setattr(Bk, "GELU_DERIV", gelu_deriv)
     tr, ref = build_pair("bf16", dropout=0.0)
     compare_step(tr, ref, tiny_batch(3, seed=4), loss_tol=5e-2, grad_rtol=0.1)
 

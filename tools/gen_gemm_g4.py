@@ -169,7 +169,8 @@ __global__ void __launch_bounds__(256) gemm_g4_kernel(const bf16* __restrict__ A
     const float4 b0v = *reinterpret_cast<const float4*>(ep.bias + col), b1v = *reinterpret_cast<const float4*>(ep.bias + col + 4);
     bia[0] = b0v.x; bia[1] = b0v.y; bia[2] = b0v.z; bia[3] = b0v.w; bia[4] = b1v.x; bia[5] = b1v.y; bia[6] = b1v.z; bia[7] = b1v.w;
   }
-  constexpr bool RES = EPI == 1 || EPI == 2, DROP = EPI == 2, GELU = EPI == 3, BWD = EPI == 4;
+  constexpr bool RES = EPI == 1 || EPI == 2, DROP = EPI == 2, GELU = EPI == 3 || EPI == 5, BWD = EPI == 4 || EPI == 6;
+  constexpr bool GD = EPI == 5, MUL = EPI == 6;  // GELU_D: aux <- GELU'(z); MUL_AUX: x aux
   constexpr bool STREAM = RES || BWD;  // one bf16 operand stream read per output: residual or aux
   const uint32_t seed = DROP ? mmfd_hash_key(*ep.seed, ep.salt) : 0u;
   const int64_t ls = RES ? ep.ldr : ep.ldaux;
@@ -186,7 +187,8 @@ __global__ void __launch_bounds__(256) gemm_g4_kernel(const bf16* __restrict__ A
   // the G8 fast path's operation order (gemm_tiles.h g8_epilogue) for the modes EPI: 0 = + bias,
   // 1 = + bias + residual, 2 = + bias, dropout, + residual, 3 = + bias, GELU (pre-activation to
   // aux), 4 = (+ bias) x GELU'(aux) (the data gradient through the FFN's GELU, read from the saved
-  // pre-activation); rounded to bf16 once. Lane (r4 = lane / 16, c = lane % 16) owns rows wm*128 + 16 i +
+  // pre-activation), 5 = + bias, GELU (its derivative to aux), 6 = (+ bias) x aux (the saved
+  // derivative); rounded to bf16 once. Lane (r4 = lane / 16, c = lane % 16) owns rows wm*128 + 16 i +
   // 4 r4 + e and the 8 consecutive columns wn*128 + 8 c ..: 16 lanes load / store 256 contiguous
   // bytes of a row. A loop over the 8 row groups (the accumulator reads are per-group code, the
   // math one body: the unrolled form did not fit the instruction cache), the next group's
@@ -215,7 +217,12 @@ __global__ void __launch_bounds__(256) gemm_g4_kernel(const bf16* __restrict__ A
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = z[e][u] + bia[u];
-      if constexpr (GELU) {
+      if constexpr (GD) {
+        float d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = gelu_and_grad_f(v[u], d[u]);
+        if (ap) V8<bf16>::store(ap + ro * ep.ldaux, d);
+      } else if constexpr (GELU) {
         if (ap) V8<bf16>::store(ap + ro * ep.ldaux, v);
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = gelu_f(v[u]);
@@ -223,8 +230,13 @@ __global__ void __launch_bounds__(256) gemm_g4_kernel(const bf16* __restrict__ A
       if constexpr (BWD) {
         float t[8];
         cur[e].get(t);
+        if constexpr (MUL) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] *= gelu_grad_f(t[u]);
+          for (int u = 0; u < 8; ++u) v[u] *= t[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] *= gelu_grad_f(t[u]);
+        }
       }
       if constexpr (DROP) {
         const uint64_t hb = (uint64_t)(row0 + ro) * (uint64_t)N + (uint64_t)col;
@@ -281,9 +293,11 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   // time is the GELU's VALU work, which one wave per SIMD does not hide better than two;
   // profiles/r05_g4_schedule_ab.log): left on gemm256_kernel unless MMFD_G4_GELU=1
   else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f && mode == 2) epi = 3;
+  else if (e.act == MMFD_ACT_GELU_D && !e.residual && e.p <= 0.0f && mode == 2) epi = 5;
   // the FFN's data gradient through GELU (x GELU'(pre-activation)): the product of dY with the
   // K-contiguous (transposed) weight copy, blocks.linear_dx
   else if (e.act == MMFD_ACT_GELU_BWD && e.aux && !e.residual && e.p <= 0.0f) epi = 4;
+  else if (e.act == MMFD_ACT_MUL_AUX && e.aux && !e.residual && e.p <= 0.0f) epi = 6;  // (its GELU_D form)
   if (epi < 0) return false;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al16(a.A) || !al16(a.B) || !al16(a.C)) return false;
@@ -299,7 +313,9 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   else if (epi == 1) G4_LAUNCH(1);
   else if (epi == 2) G4_LAUNCH(2);
   else if (epi == 3) G4_LAUNCH(3);
-  else G4_LAUNCH(4);
+  else if (epi == 4) G4_LAUNCH(4);
+  else if (epi == 5) G4_LAUNCH(5);
+  else G4_LAUNCH(6);
 #undef G4_LAUNCH
   return true;
 }
