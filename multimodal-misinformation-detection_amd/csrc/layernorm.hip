@@ -1,4 +1,4 @@
-// LayerNorm forward / backward (one wave per row, width <= 1024, width % 4 == 0).
+// LayerNorm forward / backward (one or two rows per wave, width <= 1024, width % 4 == 0).
 // Replaces nn.LayerNorm in the fusion head (model.py:39-46, 155-162; eps 1e-5) and the BERT/ViT
 // LayerNorms (eps 1e-12). Statistics in fp32; gamma/beta gradients via a deterministic two-pass
 // column reduction (per-lane column ownership -> per-block partials -> final sum).
@@ -199,42 +199,54 @@ __device__ __forceinline__ void load_f32xN(const float* p, float (&v)[VN<T>::N])
   }
 }
 
-template <typename T>
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LPR lanes per row (64 / LPR rows per wave), CH 16-B chunks per lane (lane l owns chunks l + LPR j):
+// <T, 64, VN<T>::MAXV> is the row-per-wave form for any width <= 1024; bf16 rows of 33-128 chunks
+// (width 264-1024: BERT / ViT-B's 768 = 96 chunks) run <bf16, 32, 3 | 4>, two rows per wave and no
+// idle lanes (the row-per-wave form left half the lanes of its second chunk idle at 96 chunks and
+// moved 1.5 KB per wave)
+template <typename T, int LPR, int CH>
 __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, const T* __restrict__ x, int64_t ldx,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, T* __restrict__ y, int64_t ldy,
                                                        float* __restrict__ mean, float* __restrict__ rstd,
                                                        const T* __restrict__ res = nullptr, int64_t ldr = 0,
                                                        bf16* __restrict__ pl = nullptr, int64_t pl_stride = 0) {
-  constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  constexpr int N = VN<T>::N, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, l = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  if (row >= rows) return;  // whole LPR groups leave together: the group shuffles stay inside live lanes
   const int nch = width / N;
-  float v[MAXV][N];
+  float v[CH][N];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + 64 * j;
+  for (int j = 0; j < CH; ++j) {
+    const int c = l + LPR * j;
     if (c < nch) {
       VN<T>::load(x + row * ldx + N * c, v[j]);
 #pragma unroll
       for (int e = 0; e < N; ++e) s += v[j][e];
     }
   }
-  const float mu = wave_sum(s) / (float)width;
+  const float mu = group_sum<LPR>(s) / (float)width;
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + 64 * j;
+  for (int j = 0; j < CH; ++j) {
+    const int c = l + LPR * j;
     if (c < nch)
 #pragma unroll
       for (int e = 0; e < N; ++e) { const float d = v[j][e] - mu; q += d * d; }
   }
-  const float rs = rsqrtf(wave_sum(q) / (float)width + eps);
+  const float rs = rsqrtf(group_sum<LPR>(q) / (float)width + eps);
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + 64 * j;
+  for (int j = 0; j < CH; ++j) {
+    const int c = l + LPR * j;
     if (c < nch) {
       float gg[N], bb[N], o[N];
       load_f32xN<T>(gamma + N * c, gg);
@@ -250,35 +262,44 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(int64_t rows, int width, 
       VN<T>::store(y + row * ldy + N * c, o);
       if constexpr (sizeof(T) == 4) {
         if (pl) {  // fp32: the output's split planes (hi, mid, lo) for split-operand GEMMs
-          bf16 h[N], m[N], l[N];
+          bf16 h[N], m[N], lo[N];
 #pragma unroll
           for (int e = 0; e < N; ++e) {
             h[e] = (bf16)o[e];
             const float r1 = o[e] - (float)h[e];
             m[e] = (bf16)r1;
-            l[e] = (bf16)(r1 - (float)m[e]);
+            lo[e] = (bf16)(r1 - (float)m[e]);
           }
           bf16* d = pl + row * width + N * c;
           *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, h);
           *reinterpret_cast<uint2*>(d + pl_stride) = __builtin_bit_cast(uint2, m);
-          *reinterpret_cast<uint2*>(d + 2 * pl_stride) = __builtin_bit_cast(uint2, l);
+          *reinterpret_cast<uint2*>(d + 2 * pl_stride) = __builtin_bit_cast(uint2, lo);
         }
       }
     }
   }
-  if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+  if (l == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// the row-per-wave or two-rows-per-wave form for a 16-B-vectorisable row of `width` elements
+// (> 32 chunks; narrower rows take ln_fwd16_narrow_kernel)
+template <typename T, typename... A>
+void launch_ln_fwd16(hipStream_t s, int64_t rows, int width, A... args) {
+  const int nch = width / VN<T>::N;
+  if (nch > 32 && nch <= 128 / (int)(sizeof(T) / 2)) {  // bf16 33-128 chunks, fp32 33-64
+    const dim3 grid((unsigned)((rows + 7) / 8));
+    if constexpr (sizeof(T) == 4) hipLaunchKernelGGL((ln_fwd16_kernel<T, 32, 2>), grid, dim3(256), 0, s, rows, width, args...);
+    else if (nch <= 96) hipLaunchKernelGGL((ln_fwd16_kernel<T, 32, 3>), grid, dim3(256), 0, s, rows, width, args...);
+    else hipLaunchKernelGGL((ln_fwd16_kernel<T, 32, 4>), grid, dim3(256), 0, s, rows, width, args...);
+    return;
+  }
+  hipLaunchKernelGGL((ln_fwd16_kernel<T, 64, VN<T>::MAXV>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, rows,
+                     width, args...);
 }
 
 // narrow rows (width / elements-per-16B <= LPR): 64 / LPR rows per wave, LPR lanes per row, one
 // 16-B chunk per lane, group reductions over the LPR lanes (the one-row-per-wave kernel leaves 3/4
 // of the lanes idle at width 128 bf16: Swinv2 stage 1, and half of them at the fusion head's 256)
-template <int LPR>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 template <typename T, int LPR>
 __global__ void __launch_bounds__(256) ln_fwd16_narrow_kernel(int64_t rows, int width, const T* __restrict__ x,
                                                               int64_t ldx, const float* __restrict__ gamma,
@@ -342,7 +363,29 @@ bool launch_ln_narrow(hipStream_t s, int64_t rows, int width, const T* x, int64_
   return false;
 }
 
-template <typename T>
+// one 16-B chunk as loaded (converted to fp32 after the next row's loads are issued)
+template <typename T> struct VR;
+template <> struct VR<float> {
+  float4 v;
+  __device__ __forceinline__ void load(const float* p) { v = *reinterpret_cast<const float4*>(p); }
+  __device__ __forceinline__ void get(float (&f)[4]) const { f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w; }
+};
+template <> struct VR<bf16> {
+  uint4 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  }
+};
+
+// backward, LPR lanes per row and CH chunks per lane as ln_fwd16_kernel; each wave walks rows with
+// a grid stride; with PF the next row's dy / x / dx_add chunks and statistics are loaded before this
+// row's reductions (one row's HBM latency per wave hidden behind the previous row's math: bf16
+// 768-wide rows 1.2-1.3x; the fp32 row-per-wave form, at 3 KB per row already, measured 1-3 %
+// slower with it — its doubled registers halve the waves per SIMD — and runs without)
+template <typename T, int LPR, int CH, bool PF = true>
 __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, const T* __restrict__ dy, int64_t lddy,
                                                        const T* __restrict__ x, int64_t ldx, const float* __restrict__ gamma,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -351,35 +394,63 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
                                                        const uint64_t* __restrict__ seedp, uint64_t salt,
                                                        float* __restrict__ part, bf16* __restrict__ pl = nullptr,
                                                        int64_t pl_stride = 0) {
-  constexpr int N = VN<T>::N, MAXV = VN<T>::MAXV;
-  __shared__ float red[4][2][512];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int N = VN<T>::N, RPW = 64 / LPR;
+  __shared__ float red[4][2][64 * N];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l = lane % LPR;
   const int nch = width / N;
   const uint64_t seed = (dx_drop && p > 0.f) ? *seedp : 0ull;
   const float keep = 1.0f / (1.0f - p);
-  float pg[MAXV][N], pb[MAXV][N];
+  float pg[CH][N], pb[CH][N], gv[CH][N];
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j)
+  for (int j = 0; j < CH; ++j) {
+    const int c = l + LPR * j;
 #pragma unroll
-    for (int e = 0; e < N; ++e) { pg[j][e] = 0.f; pb[j][e] = 0.f; }
-
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[MAXV][N], g[MAXV][N], add[MAXV][N];
+    for (int e = 0; e < N; ++e) { pg[j][e] = 0.f; pb[j][e] = 0.f; gv[j][e] = 0.f; }
+    if (PF && c < nch) load_f32xN<T>(gamma + N * c, gv[j]);  // (held across rows with PF only)
+  }
+  const int64_t rstep = (int64_t)gridDim.x * 4 * RPW;
+  int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RPW + lane / LPR;
+  VR<T> rd[CH], rx[CH], ra[CH];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    if (r < rows) {
+      nmu = mean[r];
+      nrs = rstd[r];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int c = l + LPR * j;
+        if (c < nch) {
+          rd[j].load(dy + r * lddy + N * c);
+          rx[j].load(x + r * ldx + N * c);
+          if (dx_add) ra[j].load(dx_add + r * ldadd + N * c);
+        }
+      }
+    }
+  };
+  if constexpr (PF) fetch(row);
+  for (; row < rows; row += rstep) {
+    if constexpr (!PF) fetch(row);
+    const float mu = nmu, rs = nrs;
+    float xh[CH][N], g[CH][N], add[CH][N];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      const int c = lane + 64 * j;
+    for (int j = 0; j < CH; ++j) {
+      const int c = l + LPR * j;
       if (c < nch) {
-        float d[N], gv[N];
-        VN<T>::load(dy + row * lddy + N * c, d);
-        VN<T>::load(x + row * ldx + N * c, xh[j]);
-        if (dx_add) VN<T>::load(dx_add + row * ldadd + N * c, add[j]);
-        load_f32xN<T>(gamma + N * c, gv);
+        float d[N], gq[N];
+        rd[j].get(d);
+        rx[j].get(xh[j]);
+        if (dx_add) ra[j].get(add[j]);
+        if constexpr (PF) {
+#pragma unroll
+          for (int e = 0; e < N; ++e) gq[e] = gv[j][e];
+        } else {
+          load_f32xN<T>(gamma + N * c, gq);
+        }
 #pragma unroll
         for (int e = 0; e < N; ++e) {
           xh[j][e] = (xh[j][e] - mu) * rs;
-          g[j][e] = d[e] * gv[e];
+          g[j][e] = d[e] * gq[e];
           s1 += g[j][e];
           s2 += g[j][e] * xh[j][e];
           pg[j][e] += d[e] * xh[j][e];
@@ -387,11 +458,12 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
         }
       }
     }
-    const float c1 = wave_sum(s1) / (float)width;
-    const float c2 = wave_sum(s2) / (float)width;
+    if constexpr (PF) fetch(row + rstep);
+    const float c1 = group_sum<LPR>(s1) / (float)width;
+    const float c2 = group_sum<LPR>(s2) / (float)width;
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      const int c = lane + 64 * j;
+    for (int j = 0; j < CH; ++j) {
+      const int c = l + LPR * j;
       if (c < nch) {
         float o[N];
 #pragma unroll
@@ -407,38 +479,45 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(int64_t rows, int width, 
         }
         if constexpr (sizeof(T) == 4) {
           if (pl) {  // fp32: split planes of the GEMM operand (dx_drop when present, else dx)
-            bf16 h[N], m[N], l[N];
+            bf16 h[N], m[N], lo[N];
 #pragma unroll
             for (int e = 0; e < N; ++e) {
               h[e] = (bf16)o[e];
               const float r1 = o[e] - (float)h[e];
               m[e] = (bf16)r1;
-              l[e] = (bf16)(r1 - (float)m[e]);
+              lo[e] = (bf16)(r1 - (float)m[e]);
             }
             bf16* dpl = pl + row * width + N * c;
             *reinterpret_cast<uint2*>(dpl) = __builtin_bit_cast(uint2, h);
             *reinterpret_cast<uint2*>(dpl + pl_stride) = __builtin_bit_cast(uint2, m);
-            *reinterpret_cast<uint2*>(dpl + 2 * pl_stride) = __builtin_bit_cast(uint2, l);
+            *reinterpret_cast<uint2*>(dpl + 2 * pl_stride) = __builtin_bit_cast(uint2, lo);
           }
         }
       }
     }
   }
-  // block reduction of the per-lane column partials, 64*N columns per slab
+  // block reduction of the per-lane column partials: slab j holds chunks [LPR j, LPR (j + 1)), the
+  // RPW row groups of a wave hold the same columns
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    if (64 * j >= nch) break;
+  for (int j = 0; j < CH; ++j) {
+    if (LPR * j >= nch) break;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
       red[wave][0][lane * N + e] = pg[j][e];
       red[wave][1][lane * N + e] = pb[j][e];
     }
     __syncthreads();
-    for (int cl = threadIdx.x; cl < 64 * N; cl += 256) {
-      const int col = 64 * N * j + cl;
+    for (int cl = threadIdx.x; cl < LPR * N; cl += 256) {
+      const int col = LPR * N * j + cl;
       if (col < width) {
-        const float sg = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
-        const float sb = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+        float sg = 0.f, sb = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+          for (int r = 0; r < RPW; ++r) {
+            sg += red[w][0][r * LPR * N + cl];
+            sb += red[w][1][r * LPR * N + cl];
+          }
         part[((int64_t)blockIdx.x * 2 + 0) * width + col] = sg;
         part[((int64_t)blockIdx.x * 2 + 1) * width + col] = sb;
       }
@@ -545,9 +624,9 @@ extern "C" int mmfd_layernorm_fwd(int dtype, int64_t rows, int64_t width, const 
                            : launch_ln_narrow<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps,
                                                      (float*)y, ldy, mean, rstd, nullptr, 0)) {
     } else if (dtype == MMFD_BF16)
-      hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
+      launch_ln_fwd16<bf16>(s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
     else
-      hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+      launch_ln_fwd16<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
   } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_fwd_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
   else
@@ -567,8 +646,8 @@ extern "C" int mmfd_layernorm_fwd_split(int64_t rows, int64_t width, const float
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
-  hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, x, ldx, gamma, beta, eps, y,
-                     ldy, mean, rstd, (const float*)nullptr, (int64_t)0, (bf16*)planes, rows * width);
+  launch_ln_fwd16<float>(s, rows, (int)width, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, (const float*)nullptr,
+                         (int64_t)0, (bf16*)planes, rows * width);
   MMFD_CHECK_LAUNCH("layernorm_fwd_split");
   return 0;
 }
@@ -592,11 +671,11 @@ extern "C" int mmfd_layernorm_fwd_res(int dtype, int64_t rows, int64_t width, co
                          : launch_ln_narrow<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps,
                                                    (float*)y, ldy, mean, rstd, (const float*)res, ldr)) {
   } else if (dtype == MMFD_BF16)
-    hipLaunchKernelGGL((ln_fwd16_kernel<bf16>), grid, dim3(256), 0, s, rows, (int)width, (const bf16*)x, ldx, gamma, beta,
-                       eps, (bf16*)y, ldy, mean, rstd, (const bf16*)res, ldr);
+    launch_ln_fwd16<bf16>(s, rows, (int)width, (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd,
+                          (const bf16*)res, ldr);
   else
-    hipLaunchKernelGGL((ln_fwd16_kernel<float>), grid, dim3(256), 0, s, rows, (int)width, (const float*)x, ldx, gamma,
-                       beta, eps, (float*)y, ldy, mean, rstd, (const float*)res, ldr);
+    launch_ln_fwd16<float>(s, rows, (int)width, (const float*)x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd,
+                           (const float*)res, ldr);
   MMFD_CHECK_LAUNCH("layernorm_fwd_res");
   return 0;
 }
@@ -709,15 +788,28 @@ int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, i
       if (nch16 <= 16) LNB(float, 16); else LNB(float, 32);
     }
 #undef LNB
+  } else if (v16 && nch16 <= (dtype == MMFD_BF16 ? 128 : 64)) {
+    // two rows per wave (ln_fwd16_kernel's comment)
+    nblocks = (int)std::min<int64_t>((rows + 7) / 8, 2048);
+    if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
+#define LNB2(T, CH) hipLaunchKernelGGL((ln_bwd16_kernel<T, 32, CH>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, \
+                                       (const T*)dy, lddy, (const T*)x, ldx, gamma, mean, rstd, (T*)dx, lddx,          \
+                                       (const T*)dx_add, ldadd, (T*)dx_drop, p, thr, seed, salt, (float*)workspace,    \
+                                       planes, rows * width)
+    if (dtype == MMFD_F32) LNB2(float, 2);
+    else if (nch16 <= 96) LNB2(bf16, 3);
+    else LNB2(bf16, 4);
+#undef LNB2
   } else if (v16) {
     if (dtype == MMFD_BF16)
-      hipLaunchKernelGGL((ln_bwd16_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
-                         (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd,
-                         (bf16*)dx_drop, p, thr, seed, salt, (float*)workspace);
+      hipLaunchKernelGGL((ln_bwd16_kernel<bf16, 64, 2>), dim3(nblocks), dim3(256), 0, s, rows, (int)width,
+                         (const bf16*)dy, lddy, (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx,
+                         (const bf16*)dx_add, ldadd, (bf16*)dx_drop, p, thr, seed, salt, (float*)workspace);
     else
-      hipLaunchKernelGGL((ln_bwd16_kernel<float>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const float*)dy,
-                         lddy, (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx, (const float*)dx_add, ldadd,
-                         (float*)dx_drop, p, thr, seed, salt, (float*)workspace, planes, rows * width);
+      hipLaunchKernelGGL((ln_bwd16_kernel<float, 64, 4, false>), dim3(nblocks), dim3(256), 0, s, rows, (int)width,
+                         (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (float*)dx, lddx,
+                         (const float*)dx_add, ldadd, (float*)dx_drop, p, thr, seed, salt, (float*)workspace, planes,
+                         rows * width);
   } else if (dtype == MMFD_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, (const bf16*)dy, lddy,
                        (const bf16*)x, ldx, gamma, mean, rstd, (bf16*)dx, lddx, (const bf16*)dx_add, ldadd, (bf16*)dx_drop,

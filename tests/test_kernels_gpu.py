@@ -587,9 +587,13 @@ def test_deberta_bias_kernels():
 # LayerNorm / misc
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("width,eps", [(256, 1e-5), (768, 1e-12), (384, 1e-5)])
-def test_layernorm(dtype, width, eps):
-    R = 1000
+@pytest.mark.parametrize("width,eps,R", [(256, 1e-5, 1000), (768, 1e-12, 1000), (384, 1e-5, 1000), (520, 1e-5, 1001),
+                                         (1024, 1e-12, 999), (768, 1e-12, 20011)])
+def test_layernorm(dtype, width, eps, R):
+    """row-per-wave (fp32, bf16 > 128 chunks), two-rows-per-wave (bf16 33-128 chunks: 520 = 65 chunks
+    with a partial third, 768 = 96, 1024 = 128) and narrow forms; odd row counts (a half-wave row
+    group alone at the end), and more rows than the backward's grid (the grid-stride loop with the
+    next row prefetched)"""
     x = _rand(R, width, dtype=dtype, seed=30, scale=2.0) + 0.5
     g = _rand(width, seed=31) * 0.1 + 1.0
     b = _rand(width, seed=32) * 0.1
