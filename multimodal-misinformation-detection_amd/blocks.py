@@ -10,6 +10,7 @@ their gradients inside the GEMM epilogue).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -38,13 +39,37 @@ def side_stream(device):
 # refreshes in the same kernel that updates the parameter (mmfd_adamw's param_bf16), so the
 # weights are cast once, not once per step. Any other in-place update of a parameter (load_state_dict,
 # torch optimizers, manual edits) bumps its version counter, and the shadow is re-cast.
+# Entries: data_ptr -> (bf16 view, (id(store), key), weakref(store)). When a module dies its store's
+# finalizer drops its entries (the bf16 copies are freed with it), and live_shadow() ignores any
+# entry whose store is gone — the allocator hands the pointers to the next model's weights, which must
+# get shadows of their own instead of AdamW writing into a dead model's copies.
 SHADOW_OF = {}
+
+
+class _ShadowStore(dict):
+    """a module's shadow store (a dict that SHADOW_OF can hold weakly)"""
+
+
+def live_shadow(ptr):
+    """SHADOW_OF[ptr] if its owning store is still alive, else None (and the stale entry is removed)"""
+    e = SHADOW_OF.get(ptr)
+    if e is not None and e[2]() is None:
+        del SHADOW_OF[ptr]
+        return None
+    return e
+
+
+def _drop_dead_store(sid):
+    """a store's finalizer: its SHADOW_OF entries go with it (the bf16 copies are freed with the module)"""
+    for ptr in [k for k, v in SHADOW_OF.items() if v[1][0] == sid and v[2]() is None]:
+        del SHADOW_OF[ptr]
 
 
 def shadow_store(module):
     st = module.__dict__.get("_mmfd_shadows")
     if st is None:
-        st = module.__dict__["_mmfd_shadows"] = {}
+        st = module.__dict__["_mmfd_shadows"] = _ShadowStore()
+        weakref.finalize(st, _drop_dead_store, id(st))
     return st
 
 
@@ -126,7 +151,7 @@ class StepCtx:
         t, members = ent
         for n, ptr, ver in members:
             src = self.P[n]
-            if src.data_ptr() != ptr or src._version != ver or SHADOW_OF.get(ptr) is None:
+            if src.data_ptr() != ptr or src._version != ver or live_shadow(ptr) is None:
                 return None
         return t
 
@@ -138,14 +163,15 @@ class StepCtx:
         for n in pnames:
             src = self.P[n]
             ptr = src.data_ptr()
-            owner = SHADOW_OF.get(ptr)
+            owner = live_shadow(ptr)
             if owner is not None and owner[1] != (id(self.shadows), key):
                 return  # shadowed elsewhere: this key is re-cast every step
             views.append((ptr, t[r:r + src.shape[0]]))
             members.append((n, ptr, src._version))
             r += src.shape[0]
+        ref = weakref.ref(self.shadows) if isinstance(self.shadows, _ShadowStore) else (lambda: self.shadows)
         for ptr, v in views:
-            SHADOW_OF[ptr] = (v, (id(self.shadows), key))
+            SHADOW_OF[ptr] = (v, (id(self.shadows), key), ref)
         self.shadows[key] = (t, members)
 
     def w(self, name):

@@ -181,6 +181,7 @@ conv_mfma_kernel(const T* __restrict__ X, const T* __restrict__ B, int64_t ldb, 
   gemm_mfma_body<T, 0, 0, TC, true, BNT>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, cg);
 }
 
+// split-K reduce, one output per thread (outputs that are not 16-B vectorisable; else splitk_reduce8_kernel)
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
                                      int64_t ldc, int64_t M, int64_t N, EpiArgs e, const float* __restrict__ rs_part,
@@ -195,18 +196,51 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, T
       rs_out[m] = (rs_beta != 0.f ? rs_beta * rs_out[m] : 0.f) + t;
     }
   }
-  if (e.vec && (N % 8) == 0) {
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total / 8; g += (int64_t)gridDim.x * blockDim.x) {
-      float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      int s = 0;
-      // four slabs' loads in flight before their adds (the adds stay in split order: same sums)
-      for (; s + 4 <= splits; s += 4) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float z = 0.f;
+    for (int s = 0; s < splits; ++s) z += ws[(int64_t)s * total + idx];
+    epilogue_store<TC>(e, C, ldc, N, idx / N, idx % N, z, seed);
+  }
+}
+
+// split-K reduce for 16-B-aligned outputs with N % 8 == 0: 8 consecutive outputs per thread group,
+// the splits cut into P contiguous ranges summed by P threads (each in split order) and combined
+// through LDS in range order — deterministic, and P x the threads of one-thread-per-8-outputs: a
+// weight gradient's 768 x 768 output is 73,728 groups, 288 busy blocks on 256 CUs at P = 1 (the
+// slab reads ran at ~1 TB/s), 2,304 at P = 8
+template <typename TC, int P>
+__global__ void __launch_bounds__(256) splitk_reduce8_kernel(const float* __restrict__ ws, int splits,
+                                                             TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N,
+                                                             EpiArgs e, const float* __restrict__ rs_part,
+                                                             int rs_nparts, float* __restrict__ rs_out, float rs_beta) {
+  constexpr int G = 256 / P;  // output groups per block pass
+  __shared__ float red[P > 1 ? P - 1 : 1][G][9];
+  const uint32_t seed = (e.p > 0.0f) ? mmfd_hash_key(*e.seed, e.salt) : 0u;  // dropout hash key
+  const int64_t total = M * N, groups = total / 8;
+  if (rs_part) {  // the fused row sums' per-split partials (G8 split-K), summed in split order
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+      float t = 0.f;
+      for (int s = 0; s < rs_nparts; ++s) t += rs_part[(int64_t)s * M + m];
+      rs_out[m] = (rs_beta != 0.f ? rs_beta * rs_out[m] : 0.f) + t;
+    }
+  }
+  const int gi = threadIdx.x % G, pi = threadIdx.x / G;
+  const int per = (splits + P - 1) / P;
+  const int s0 = pi * per, s1 = min(splits, s0 + per);
+  for (int64_t gb = (int64_t)blockIdx.x * G; gb < groups; gb += (int64_t)gridDim.x * G) {
+    const int64_t g = gb + gi;
+    float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (g < groups) {
+      const float* base = ws + g * 8;
+      int s = s0;
+      for (; s + 4 <= s1; s += 4) {  // four slabs' loads in flight before their adds (split order)
         float4 a[4], b[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float* p = ws + (int64_t)(s + u) * total + g * 8;
-          a[u] = *reinterpret_cast<const float4*>(p);
-          b[u] = *reinterpret_cast<const float4*>(p + 4);
+          const float* q = base + (int64_t)(s + u) * total;
+          a[u] = *reinterpret_cast<const float4*>(q);
+          b[u] = *reinterpret_cast<const float4*>(q + 4);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -214,20 +248,27 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, T
           z[4] += b[u].x; z[5] += b[u].y; z[6] += b[u].z; z[7] += b[u].w;
         }
       }
-      for (; s < splits; ++s) {
-        const float* p = ws + (int64_t)s * total + g * 8;
-        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      for (; s < s1; ++s) {
+        const float* q = base + (int64_t)s * total;
+        const float4 a = *reinterpret_cast<const float4*>(q), b = *reinterpret_cast<const float4*>(q + 4);
         z[0] += a.x; z[1] += a.y; z[2] += a.z; z[3] += a.w; z[4] += b.x; z[5] += b.y; z[6] += b.z; z[7] += b.w;
       }
-      epilogue_store8<TC>(e, C, ldc, N, (g * 8) / N, (g * 8) % N, z, seed);
     }
-    return;
-  }
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    float z = 0.f;
-    for (int s = 0; s < splits; ++s) z += ws[(int64_t)s * total + idx];
-    epilogue_store<TC>(e, C, ldc, N, idx / N, idx % N, z, seed);
+    if constexpr (P > 1) {
+      if (pi > 0) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) red[pi - 1][gi][u] = z[u];
+      }
+      __syncthreads();
+      if (pi == 0) {
+#pragma unroll
+        for (int q = 0; q < P - 1; ++q)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) z[u] += red[q][gi][u];
+      }
+      __syncthreads();
+    }
+    if (pi == 0 && g < groups) epilogue_store8<TC>(e, C, ldc, N, (g * 8) / N, (g * 8) % N, z, seed);
   }
 }
 
@@ -722,14 +763,29 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   MMFD_CHECK_LAUNCH("gemm_mfma");
   if (ws) {
     const int64_t total = a.M * a.N;
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
     // the row sums' partials (rs_mode 2 / 3) are reduced by the same launch
     const float* rsp = rs_mode >= 2 ? rs_part : nullptr;
+    if (e.vec && a.N % 8 == 0) {
+      // split ranges per group: up to 8, while the threads stay under ~2^19 (2,048 per CU)
+      const int64_t groups = total / 8;
+      int P = 1;
+      while (P < 8 && 2 * P <= splits && groups * P < ((int64_t)1 << 19)) P *= 2;
+      const int G = 256 / P;
+      const int blocks = (int)std::min<int64_t>(std::max<int64_t>((groups + G - 1) / G, (a.M + 255) / 256), 16384);
+#define SKR(TC, PP) hipLaunchKernelGGL((splitk_reduce8_kernel<TC, PP>), dim3(blocks), dim3(256), 0, s, ws, splits, \
+                                       (TC*)a.C, a.ldc, a.M, a.N, e, rsp, rs_nparts, a.a_rowsum, a.a_rowsum_beta)
+      if (cbf) { if (P == 8) SKR(bf16, 8); else if (P == 4) SKR(bf16, 4); else if (P == 2) SKR(bf16, 2); else SKR(bf16, 1); }
+      else { if (P == 8) SKR(float, 8); else if (P == 4) SKR(float, 4); else if (P == 2) SKR(float, 2); else SKR(float, 1); }
+#undef SKR
+      MMFD_CHECK_LAUNCH("splitk_reduce");
+    } else {
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
     if (cbf) hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, s, ws, splits, (bf16*)a.C, a.ldc,
                                 a.M, a.N, e, rsp, rs_nparts, a.a_rowsum, a.a_rowsum_beta);
     else hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(256), 0, s, ws, splits, (float*)a.C, a.ldc,
                             a.M, a.N, e, rsp, rs_nparts, a.a_rowsum, a.a_rowsum_beta);
     MMFD_CHECK_LAUNCH("splitk_reduce");
+    }
   } else if (rs_mode == 3) {  // no split-K: only the column tiles' row-sum partials to reduce
     hipLaunchKernelGGL(mmfd_reduce_partials_kernel, dim3((unsigned)((a.M + 63) / 64)), dim3(1024), 0, s,
                        (const float*)rs_part, rs_nparts, a.M, a.M, a.a_rowsum, a.a_rowsum_beta);

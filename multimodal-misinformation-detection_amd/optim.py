@@ -43,10 +43,10 @@ class AdamW(torch.optim.Optimizer):
         self._tables = {}
 
     def _table(self, entries, device):
-        from .blocks import SHADOW_OF
+        from .blocks import live_shadow
         shadows = []
         for p, *_ in entries:  # the bf16 weight copies the HIP modules read (refreshed in the same launch)
-            sh = SHADOW_OF.get(p.data_ptr())
+            sh = live_shadow(p.data_ptr())
             ok = sh is not None and sh[0].dtype == torch.bfloat16 and sh[0].numel() == p.numel()
             shadows.append(sh[0].data_ptr() if ok else 0)
         key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s.data_ptr(), p.numel(), sp)
@@ -91,11 +91,11 @@ class AdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def finalize_capture(self):
-        from .blocks import SHADOW_OF
+        from .blocks import live_shadow
         for t, entries in getattr(self, "_pending_capture", []):
             arr = (K.AdamWTensor * len(entries))()
             for i, (p, g, m, v, st) in enumerate(entries):
-                sh = SHADOW_OF.get(p.data_ptr())
+                sh = live_shadow(p.data_ptr())
                 ok = sh is not None and sh[0].dtype == torch.bfloat16 and sh[0].numel() == p.numel()
                 arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
                 arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()

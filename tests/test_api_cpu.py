@@ -326,3 +326,29 @@ def test_best_model_checkpoint_with_numpy_metric_loads(tmp_path, numpy1):
     torch.save({"model_state_dict": m.state_dict(), "x": io.BytesIO}, bad)
     with pytest.raises(Exception):
         load_checkpoint(bad)
+
+
+def test_stale_shadow_entries_expire_with_their_store():
+    """blocks.SHADOW_OF entries whose module (shadow store) is gone are dropped by live_shadow, so a
+    reused weight pointer is not treated as already shadowed"""
+    import gc
+    from mmfd import blocks as Bk
+
+    class M:
+        pass
+
+    m = M()
+    st = Bk.shadow_store(m)
+    ptr = 0x7fff0000
+    import weakref
+    Bk.SHADOW_OF[ptr] = (None, (id(st), "w"), weakref.ref(st))
+    Bk.SHADOW_OF[ptr + 64] = (None, (id(st), "w"), weakref.ref(st))
+    assert Bk.live_shadow(ptr) is not None
+    del m, st
+    gc.collect()
+    # the store's finalizer dropped both entries; a stale entry found later is dropped on lookup
+    assert ptr not in Bk.SHADOW_OF and ptr + 64 not in Bk.SHADOW_OF
+    dead = Bk._ShadowStore()
+    Bk.SHADOW_OF[ptr] = (None, (id(dead), "w"), weakref.ref(dead))
+    del dead
+    assert Bk.live_shadow(ptr) is None and ptr not in Bk.SHADOW_OF

@@ -120,6 +120,43 @@ def test_bf16_weight_shadows_follow_adamw_and_external_updates():
         assert sc._shadow(k, names) is None
 
 
+def test_bf16_shadows_registered_again_after_model_replaced():
+    """a model built after another was freed (the allocator hands its weight pointers to the new
+    model) gets its bf16 weight copies registered — the dead model's SHADOW_OF entries are stale,
+    not owners — and AdamW refreshes the new copies (blocks.live_shadow)"""
+    import gc
+    from mmfd import blocks as Bk
+
+    def registered(tr):
+        return sum(len(mem) for m in (tr.text_encoder, tr.image_encoder, tr.head)
+                   for key, (t, mem) in Bk.shadow_store(m).items() if not isinstance(key, tuple))
+
+    tr, _ = build_pair("bf16", dropout=0.0)
+    tr.step({k: v.cuda() for k, v in tiny_batch(2, seed=50).items()})
+    torch.cuda.synchronize()
+    n0 = registered(tr)
+    assert n0 > 20
+    del tr
+    gc.collect()
+    tr2, _ = build_pair("bf16", dropout=0.0)
+    for s in range(2):
+        tr2.step({k: v.cuda() for k, v in tiny_batch(2, seed=51 + s).items()})
+    torch.cuda.synchronize()
+    assert registered(tr2) == n0
+    assert all(e[2]() is not None for e in Bk.SHADOW_OF.values())
+    from mmfd import kernels as K
+    for m in (tr2.text_encoder, tr2.image_encoder, tr2.head):
+        P = dict(m.named_parameters())
+        for key, (t, members) in Bk.shadow_store(m).items():
+            if isinstance(key, tuple):
+                continue
+            r = 0
+            for n, ptr, ver in members:
+                rows = P[n].shape[0]
+                assert torch.equal(t[r:r + rows].reshape(-1), K.cast(P[n].detach().reshape(-1), torch.bfloat16)), key
+                r += rows
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_captured_step_replays_equal_eager_steps(precision):
     """FusionTrainer.capture/replay (the whole step as one HIP graph: dropout seeds advance on the
