@@ -150,9 +150,9 @@ int mmfd_set_fp32_gemm_mode(int mode);
    planes (mmfd.kernels.x6_ok) asks this, so it honours every switch the library does. */
 int mmfd_gemm_runs_split(const mmfd_gemm_args* args);
 /* the four-wave assembly-scheduled bf16 forward GEMM (gemm_g4.hip): mode 0 = off (those products run
-   on the 256x256 eight-wave kernel), 1 = on for the bias / residual / dropout + residual epilogues
-   (default), 2 = also the GELU + pre-activation epilogue; -1 only queries. Load-time defaults from
-   env MMFD_G4=0 / MMFD_G4_GELU=1. Returns the previous mode (A/B measurements and tests; not per
+   on the 256x256 eight-wave kernel), 1 = on for the bias / residual / dropout + residual epilogues,
+   2 = also the GELU epilogues (default); -1 only queries. Load-time defaults from env MMFD_G4=0 /
+   MMFD_G4_GELU=0. Returns the previous mode (A/B measurements and tests; not per
    stream: set it between launches). */
 int mmfd_set_g4_mode(int mode);
 /* the largest K the four-wave GEMM takes (default 1024, env MMFD_G4_KMAX); kmax <= 0 only queries.

@@ -377,8 +377,8 @@ _G4_MODES = {"off": 0, "on": 1, "gelu": 2}
 
 
 def set_g4_mode(mode=None, kmax=None):
-    """The four-wave bf16 forward GEMM (gemm_g4.hip): 'off', 'on' (default) or 'gelu' (the FFN1 GELU
-    epilogue too), and the largest K it takes. Returns the previous (mode, kmax); None leaves a
+    """The four-wave bf16 forward GEMM (gemm_g4.hip): 'off', 'on' or 'gelu' (default: the FFN1 GELU
+    epilogues too), and the largest K it takes. Returns the previous (mode, kmax); None leaves a
     setting as it is (A/B measurements and tests: set between launches, not per stream)."""
     old = lib().mmfd_set_g4_mode(-1 if mode is None else _G4_MODES[mode])
     _check(0 if old >= 0 else old, "mmfd_set_g4_mode")

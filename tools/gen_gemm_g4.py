@@ -265,11 +265,12 @@ namespace mmfd_gemmx {
 // the products the four-wave kernel takes: bf16 x bf16 -> bf16, both operands K-contiguous (the
 // nn.Linear forward), full tiles, alpha 1 and at most a bias in the epilogue; env MMFD_G4=0 sends
 // them to gemm256_kernel (A/B measurements, tests). The switches are read from the environment once,
-// when the library loads (MMFD_G4=0: off; MMFD_G4_GELU=1: the FFN1 GELU mode too; MMFD_G4_KMAX), and
+// when the library loads (MMFD_G4=0: off; MMFD_G4_GELU=0: not the FFN1 GELU modes; MMFD_G4_KMAX), and
 // changed at run time only through mmfd_set_g4_mode / mmfd_set_g4_kmax — never a getenv per launch
 int g_g4_mode = [] {
   const char* v = getenv("MMFD_G4");
-  return (v && v[0] == '0') ? 0 : getenv("MMFD_G4_GELU") ? 2 : 1;
+  const char* g = getenv("MMFD_G4_GELU");
+  return (v && v[0] == '0') ? 0 : (g && g[0] == '0') ? 1 : 2;
 }();
 int64_t g_g4_kmax = [] {
   const char* k = getenv("MMFD_G4_KMAX");
@@ -289,9 +290,10 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   int epi = -1;
   if (e.act == MMFD_ACT_NONE && !e.residual && e.p <= 0.0f) epi = 0;                    // QKV
   else if (e.act == MMFD_ACT_NONE && e.residual && !e.res_first) epi = e.p > 0.0f ? 2 : 1;  // out / FFN2
-  // FFN1 (bias + GELU + pre-activation): measured 0.89-1.03x of gemm256_kernel across boxes (its
-  // time is the GELU's VALU work, which one wave per SIMD does not hide better than two;
-  // profiles/r05_g4_schedule_ab.log): left on gemm256_kernel unless MMFD_G4_GELU=1
+  // FFN1 (bias + GELU [+ its derivative or the pre-activation to aux]): mode 2, the default since
+  // the derivative-saving form (EPI 5, the training FFN1): bf16 step +0.8 % on two boxes
+  // (profiles/r06n_g4_gelu_ab.log; the pre-activation form measured 0.89-1.03x of gemm256_kernel per
+  // GEMM across boxes in round 5, profiles/r05_g4_schedule_ab.log)
   else if (e.act == MMFD_ACT_GELU && !e.residual && e.p <= 0.0f && mode == 2) epi = 3;
   else if (e.act == MMFD_ACT_GELU_D && !e.residual && e.p <= 0.0f && mode == 2) epi = 5;
   // the FFN's data gradient through GELU (x GELU'(pre-activation)): the product of dY with the
