@@ -155,6 +155,10 @@ int mmfd_gemm_runs_split(const mmfd_gemm_args* args);
    MMFD_G4_GELU=0. Returns the previous mode (A/B measurements and tests; not per
    stream: set it between launches). */
 int mmfd_set_g4_mode(int mode);
+/* the four-wave GEMM's grid: 1 = persistent (one workgroup per CU walking its tiles, the next tile's
+   first K-tiles loaded during this tile's epilogue; default), 0 = one workgroup per tile (env
+   MMFD_G4_PERSIST=0); -1 only queries. Returns the previous setting. */
+int mmfd_set_g4_persist(int on);
 /* the largest K the four-wave GEMM takes (default 1024, env MMFD_G4_KMAX); kmax <= 0 only queries.
    Returns the previous limit. */
 int64_t mmfd_set_g4_kmax(int64_t kmax);

@@ -142,6 +142,7 @@ SIGNATURES = {
     "mmfd_gemm_splits": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_gemm_runs_split": (_I, [ctypes.POINTER(GemmArgs)]),
     "mmfd_set_g4_mode": (_I, [_I]),
+    "mmfd_set_g4_persist": (_I, [_I]),
     "mmfd_transpose": (_I, [_I, _I64, _I64, _VP, _I64, _VP, _I64, _VP]),
     "mmfd_set_g4_kmax": (_I64, [_I64]),
     "mmfd_split3": (_I, [_I64, _I64, _VP, _I64, _VP, _VP]),
@@ -384,6 +385,14 @@ def set_g4_mode(mode=None, kmax=None):
     _check(0 if old >= 0 else old, "mmfd_set_g4_mode")
     old_k = lib().mmfd_set_g4_kmax(0 if kmax is None else int(kmax))
     return {v: k for k, v in _G4_MODES.items()}[old], int(old_k)
+
+
+def set_g4_persist(on=None):
+    """the four-wave GEMM's persistent grid (default True) or one workgroup per tile; returns the
+    previous setting (None only queries)"""
+    old = lib().mmfd_set_g4_persist(-1 if on is None else int(bool(on)))
+    _check(0 if old >= 0 else old, "mmfd_set_g4_persist")
+    return bool(old)
 
 
 def g4_mode():

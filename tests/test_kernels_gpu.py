@@ -85,9 +85,10 @@ def test_gemm_bf16_g8_ktile_counts(layout, Kd):
 @pytest.fixture
 def g4_restore():
     """the four-wave GEMM switches (mmfd_set_g4_mode / _kmax) as they were before the test"""
-    old = K.g4_mode()
+    old, persist = K.g4_mode(), K.set_g4_persist()
     yield
     K.set_g4_mode(*old)
+    K.set_g4_persist(persist)
 
 
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 128), (768, 2304, 768), (1024, 512, 1024),
@@ -189,6 +190,46 @@ def test_gemm_bf16_g4_strided_views_match_g8(Kd, mode, g4_restore):
     if mode != "dropout_residual":
         err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 8e-3, err
+
+
+# tile counts past one per CU (the persistent grid walks several tiles per workgroup; 297 is not a
+# multiple of 8, so the XCD-contiguous order is off), every epilogue mode
+@pytest.mark.parametrize("shape", [(8192, 2304, 768), (256 * 33, 2304, 128), (2048, 3072, 64)])
+@pytest.mark.parametrize("mode", ["bias", "residual", "dropout_residual", "gelu_aux", "gelu_deriv", "gelu_bwd",
+                                  "mul_aux", "gelu_noaux"])
+def test_gemm_bf16_g4_persistent_matches_g8(shape, mode, g4_restore):
+    """the persistent four-wave GEMM (next tile's first K-tiles in flight during this tile's
+    epilogue) gives the same bits as one workgroup per tile and as gemm256_kernel"""
+    M, N, Kd = shape
+    A = _rand(M, Kd, dtype=torch.bfloat16, seed=81).to(DEV)
+    B = _rand(N, Kd, dtype=torch.bfloat16, seed=82).to(DEV)
+    bias = _rand(N, seed=83).to(DEV)
+    res = _rand(M, N, dtype=torch.bfloat16, seed=84).to(DEV)
+    outs = []
+    for g4, persist in (("gelu", True), ("gelu", False), ("off", True)):
+        K.set_g4_mode(g4)
+        K.set_g4_persist(persist)
+        aux = res.clone() if mode in ("gelu_bwd", "mul_aux") else torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        kw = dict(bias=bias)
+        if mode == "residual":
+            kw.update(residual=res)
+        elif mode == "dropout_residual":
+            kw.update(residual=res, dropout_p=0.1, seed=K.Seed(79, device=DEV), salt=7)
+        elif mode == "gelu_aux":
+            kw.update(act=K.ACT_GELU, aux=aux)
+        elif mode == "gelu_deriv":
+            kw.update(act=K.ACT_GELU_D, aux=aux)
+        elif mode == "gelu_bwd":
+            kw = dict(act=K.ACT_GELU_BWD, aux=aux)
+        elif mode == "mul_aux":
+            kw = dict(act=K.ACT_MUL_AUX, aux=aux)
+        else:
+            kw.update(act=K.ACT_GELU)
+        outs.append((K.gemm(A, B, **kw), aux))
+    torch.cuda.synchronize()
+    for o, x in outs[1:]:
+        assert torch.equal(outs[0][0], o), (outs[0][0].float() - o.float()).abs().max().item()
+        assert torch.equal(outs[0][1], x)
 
 
 @pytest.mark.parametrize("mode", ["gelu_aux", "gelu_deriv", "residual", "dropout_residual"])
