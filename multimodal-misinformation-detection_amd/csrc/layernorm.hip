@@ -752,6 +752,13 @@ __global__ void __launch_bounds__(1024) ln_gb_reduce_kernel(const float* __restr
 
 
 namespace {
+// backward blocks (A/B: env MMFD_LN_BWD_BLOCKS, read once at load)
+const int g_ln_bwd_blocks = [] {
+  const char* v = getenv("MMFD_LN_BWD_BLOCKS");
+  const int n = v ? atoi(v) : 0;
+  return n > 0 ? n : 512;
+}();
+
 int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, int64_t lddy,
                        const void* x, int64_t ldx, const float* gamma, const float* mean,
                        const float* rstd, void* dx, int64_t lddx, const void* dx_add, int64_t ldadd,
@@ -762,7 +769,10 @@ int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, i
   MMFD_CHECK_ARG(!(dx_drop && dropout_p > 0.f) || seed, "layernorm_bwd: dropout needs seed");
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  int nblocks = (int)std::min<int64_t>((rows + 3) / 4, 2048);
+  // backward grid: the kernels walk rows with a grid stride, so every resident block is busy with
+  // g_ln_bwd_blocks of them (2 per CU at their register counts); each block leaves one gamma / beta
+  // partial row, which ln_gb_reduce_kernel then sums — more blocks only add partials
+  int nblocks = (int)std::min<int64_t>((rows + 3) / 4, g_ln_bwd_blocks);
   const int64_t per = 2 * width * 4;
   if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
   MMFD_CHECK_ARG(nblocks >= 1 && workspace, "layernorm_bwd: workspace too small");
@@ -777,7 +787,7 @@ int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, i
   if (v16 && nch16 <= 32) {
     // narrow rows: RPW rows per wave, so a block covers 4 * RPW rows
     const int rpb = nch16 <= 16 ? 16 : 8;
-    nblocks = (int)std::min<int64_t>((rows + rpb - 1) / rpb, 2048);
+    nblocks = (int)std::min<int64_t>((rows + rpb - 1) / rpb, g_ln_bwd_blocks);
     if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
 #define LNB(T, LPR) hipLaunchKernelGGL((ln_bwd16_narrow_kernel<T, LPR>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, \
                                        (const T*)dy, lddy, (const T*)x, ldx, gamma, mean, rstd, (T*)dx, lddx,             \
@@ -790,7 +800,7 @@ int layernorm_bwd_impl(int dtype, int64_t rows, int64_t width, const void* dy, i
 #undef LNB
   } else if (v16 && nch16 <= (dtype == MMFD_BF16 ? 128 : 64)) {
     // two rows per wave (ln_fwd16_kernel's comment)
-    nblocks = (int)std::min<int64_t>((rows + 7) / 8, 2048);
+    nblocks = (int)std::min<int64_t>((rows + 7) / 8, g_ln_bwd_blocks);
     if (workspace_bytes < nblocks * per) nblocks = (int)(workspace_bytes / per);
 #define LNB2(T, CH) hipLaunchKernelGGL((ln_bwd16_kernel<T, 32, CH>), dim3(nblocks), dim3(256), 0, s, rows, (int)width, \
                                        (const T*)dy, lddy, (const T*)x, ldx, gamma, mean, rstd, (T*)dx, lddx,          \
