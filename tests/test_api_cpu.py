@@ -352,3 +352,16 @@ def test_stale_shadow_entries_expire_with_their_store():
     Bk.SHADOW_OF[ptr] = (None, (id(dead), "w"), weakref.ref(dead))
     del dead
     assert Bk.live_shadow(ptr) is None and ptr not in Bk.SHADOW_OF
+
+
+def test_gemm_g4_source_is_the_generator_output(tmp_path):
+    """csrc/gemm_g4.hip is generated (tools/gen_gemm_g4.py): the committed file equals a fresh run"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "gemm_g4.hip"
+    subprocess.run([sys.executable, os.path.join(root, "tools", "gen_gemm_g4.py")], check=True,
+                   env={**os.environ, "G4_OUT": str(out)}, stdout=subprocess.DEVNULL)
+    committed = os.path.join(root, "multimodal-misinformation-detection_amd", "csrc", "gemm_g4.hip")
+    assert out.read_text() == open(committed).read()
