@@ -20,6 +20,11 @@
 #include "gemm_tiles.h"
 #include "gemm256.h"
 
+namespace mmfd_gemmx {
+// the four-wave kernel's epilogue mode for this product, -1 when it does not take it (gemm_g4.hip)
+int g4_epi(const mmfd_gemm_args& a, const EpiArgs& e, int splits);
+}  // namespace mmfd_gemmx
+
 namespace {
 
 // CONV: implicit-GEMM convolution (ConvGeom): A is the NHWC activation and its fill gathers the
@@ -181,6 +186,69 @@ conv_mfma_kernel(const T* __restrict__ X, const T* __restrict__ B, int64_t ldb, 
   gemm_mfma_body<T, 0, 0, TC, true, BNT>(X, cg.C, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, cg);
 }
 
+// The epilogue activations MMFD_ACT_GELU_D (GELU, aux <- gelu'(z)) and MMFD_ACT_MUL_AUX (z *= aux)
+// run in the four-wave kernel's register epilogue (gemm_g4.hip, the bf16 training FFN), and
+// everywhere else in the split-K reduce / simple kernels only: a product with one of them that the
+// four-wave kernel does not take writes its raw fp32 sums to a workspace slab (one split at least)
+// and the reduce applies the whole epilogue. The tile kernels' shared epilogues (gemm_tiles.h) keep
+// their round-5 code — the two extra activations inlined there made every GEMM's epilogue slower
+// (config-5 extract −4 %, profiles/r06t_extract_regression.log).
+__device__ __forceinline__ bool act_ext(int act) { return act == MMFD_ACT_GELU_D || act == MMFD_ACT_MUL_AUX; }
+
+// epilogue_store (gemm_tiles.h) with the two extra activations: bias, [residual first], the
+// activation, then the unchanged tail (dropout, residual, beta, store / planes)
+template <typename TC>
+__device__ __forceinline__ void epilogue_store_x(const EpiArgs& e, TC* C, int64_t ldc, int64_t N, int64_t row,
+                                                 int64_t col, float z, uint32_t hkey) {
+  if (!act_ext(e.act)) return epilogue_store<TC>(e, C, ldc, N, row, col, z, hkey);
+  if (e.bias) z += e.bias[col];
+  if (e.res_first && e.residual) z += to_f32(reinterpret_cast<const TC*>(e.residual)[row * e.ldr + col]);
+  TC* ax = reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col;
+  if (e.act == MMFD_ACT_GELU_D) {
+    float d;
+    z = gelu_and_grad_f(z, d);
+    if (e.aux) *ax = from_f32<TC>(d);
+  } else {
+    z *= to_f32(*ax);
+  }
+  EpiArgs t = e;
+  t.act = MMFD_ACT_NONE; t.bias = nullptr;
+  if (e.res_first) t.residual = nullptr;
+  epilogue_store<TC>(t, C, ldc, N, row, col, z, hkey);
+}
+
+template <typename TC>
+__device__ __forceinline__ void epilogue_store8_x(const EpiArgs& e, TC* C, int64_t ldc, int64_t N, int64_t row,
+                                                  int64_t col, float (&z)[8], uint32_t hkey) {
+  if (!act_ext(e.act)) return epilogue_store8<TC>(e, C, ldc, N, row, col, z, hkey);
+  if (e.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col), b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
+    z[0] += b0.x; z[1] += b0.y; z[2] += b0.z; z[3] += b0.w; z[4] += b1.x; z[5] += b1.y; z[6] += b1.z; z[7] += b1.w;
+  }
+  if (e.res_first && e.residual) {
+    float r[8];
+    V8<TC>::load(reinterpret_cast<const TC*>(e.residual) + row * e.ldr + col, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] += r[q];
+  }
+  TC* ax = reinterpret_cast<TC*>(e.aux) + row * e.ldaux + col;
+  if (e.act == MMFD_ACT_GELU_D) {
+    float d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] = gelu_and_grad_f(z[q], d[q]);
+    if (e.aux) V8<TC>::store(ax, d);
+  } else {
+    float a[8];
+    V8<TC>::load(ax, a);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] *= a[q];
+  }
+  EpiArgs t = e;
+  t.act = MMFD_ACT_NONE; t.bias = nullptr;
+  if (e.res_first) t.residual = nullptr;
+  epilogue_store8<TC>(t, C, ldc, N, row, col, z, hkey);
+}
+
 // split-K reduce, one output per thread (outputs that are not 16-B vectorisable; else splitk_reduce8_kernel)
 template <typename TC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, TC* __restrict__ C,
@@ -200,7 +268,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, T
        idx += (int64_t)gridDim.x * blockDim.x) {
     float z = 0.f;
     for (int s = 0; s < splits; ++s) z += ws[(int64_t)s * total + idx];
-    epilogue_store<TC>(e, C, ldc, N, idx / N, idx % N, z, seed);
+    epilogue_store_x<TC>(e, C, ldc, N, idx / N, idx % N, z, seed);
   }
 }
 
@@ -268,7 +336,7 @@ __global__ void __launch_bounds__(256) splitk_reduce8_kernel(const float* __rest
       }
       __syncthreads();
     }
-    if (pi == 0 && g < groups) epilogue_store8<TC>(e, C, ldc, N, (g * 8) / N, (g * 8) % N, z, seed);
+    if (pi == 0 && g < groups) epilogue_store8_x<TC>(e, C, ldc, N, (g * 8) / N, (g * 8) % N, z, seed);
   }
 }
 
@@ -288,7 +356,7 @@ __global__ void gemm_simple_kernel(const T* __restrict__ A, int64_t lda, int ta,
       const float b = to_f32(tb ? B[k * ldb + n] : B[n * ldb + k]);
       s = fmaf(a, b, s);
     }
-    epilogue_store<TC>(e, C, ldc, N, m, n, alpha * s, seed);
+    epilogue_store_x<TC>(e, C, ldc, N, m, n, alpha * s, seed);
   }
 }
 
@@ -585,6 +653,37 @@ extern "C" int mmfd_debug_g8_stamps(void* host_dst, int64_t bytes) {
 }
 #endif
 
+namespace {
+EpiArgs make_epi(const mmfd_gemm_args& a) {
+  EpiArgs e;
+  e.bias = a.ep.bias; e.residual = a.ep.residual; e.ldr = a.ep.ldr; e.aux = a.ep.aux;
+  e.ldaux = a.ep.ldaux; e.act = a.ep.act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
+  e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
+  e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta; e.res_first = a.ep.residual_first ? 1 : 0;
+  e.pl = a.c_dtype == MMFD_F32 ? (bf16*)a.ep.out_planes : nullptr;
+  e.pl_stride = a.M * a.N;
+  e.c_out = (a.C != nullptr) ? 1 : 0;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  bool v = (a.C == nullptr || al(a.C)) && (a.ldc % 8) == 0;
+  if (a.ep.residual) v = v && al(a.ep.residual) && (a.ep.ldr % 8) == 0;
+  if (a.ep.aux) v = v && al(a.ep.aux) && (a.ep.ldaux % 8) == 0;
+  if (a.ep.bias) v = v && al(a.ep.bias);
+  e.vec = v ? 1 : 0;
+  return e;
+}
+
+// a GELU_D / MUL_AUX product on the MFMA paths that the four-wave kernel does not take: the tile
+// kernels write raw sums to a slab (at least one split) and the reduce runs the epilogue
+bool ext_slab(const mmfd_gemm_args& a, int splits) {
+  const int act = a.ep.act;
+  if (act != MMFD_ACT_GELU_D && act != MMFD_ACT_MUL_AUX) return false;
+  if (splits == 1 && use_g8(a) && a.dtype == MMFD_BF16 && a.c_dtype == MMFD_BF16 && !a.conv &&
+      mmfd_gemmx::g4_epi(a, make_epi(a), splits) >= 0)
+    return false;
+  return true;
+}
+}  // namespace
+
 // The queries return -1 (error string set) for arguments of another ABI layout (struct_size).
 static bool gemm_struct_ok(const mmfd_gemm_args* a, const char* what) {
   if (a && a->struct_size == (int64_t)sizeof(mmfd_gemm_args)) return true;
@@ -599,6 +698,7 @@ extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
   const X6Plan xp = x6_plan(*a);
   int64_t need = 0;
   const int splits = choose_splits(*a, &need, xp.on);
+  if (ext_slab(*a, splits) && need < a->M * a->N * 4) need = a->M * a->N * 4;
   need += rowsum_ws_bytes(*a, splits, use_g8(*a));
   if (xp.on)  // + the bf16 planes of the operands not handed over already split
     need = align256(need) + (a->a_planes ? 0 : align256(3 * xp.pa)) + (a->b_planes ? 0 : 3 * xp.pb);
@@ -648,22 +748,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   if (a.M == 0 || a.N == 0) return 0;
   MMFD_CHECK_ARG(a.K == 0 || (a.A && a.B), "mmfd_gemm: null operand");
 
-  EpiArgs e;
-  e.bias = a.ep.bias; e.residual = a.ep.residual; e.ldr = a.ep.ldr; e.aux = a.ep.aux;
-  e.ldaux = a.ep.ldaux; e.act = act; e.p = a.ep.dropout_p > 0.f ? a.ep.dropout_p : 0.f;
-  e.thr = mmfd_drop_threshold(e.p); e.keep_scale = 1.0f / (1.0f - e.p);
-  e.seed = a.ep.seed; e.salt = a.ep.salt; e.beta = a.beta; e.res_first = a.ep.residual_first ? 1 : 0;
-  e.pl = a.c_dtype == MMFD_F32 ? (bf16*)a.ep.out_planes : nullptr;
-  e.pl_stride = a.M * a.N;
-  e.c_out = (a.C != nullptr) ? 1 : 0;
-  {
-    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    bool v = (a.C == nullptr || al(a.C)) && (a.ldc % 8) == 0;
-    if (a.ep.residual) v = v && al(a.ep.residual) && (a.ep.ldr % 8) == 0;
-    if (a.ep.aux) v = v && al(a.ep.aux) && (a.ep.ldaux % 8) == 0;
-    if (a.ep.bias) v = v && al(a.ep.bias);
-    e.vec = v ? 1 : 0;
-  }
+  const EpiArgs e = make_epi(a);
 
   const bool bf = a.dtype == MMFD_BF16, cbf = a.c_dtype == MMFD_BF16;
   ConvGeom cg;
@@ -714,7 +799,15 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   const int tps = (nkt + splits - 1) / std::max(splits, 1);
   splits = tps > 0 ? (nkt + tps - 1) / tps : 1;
   if (splits < 1) splits = 1;
-  float* ws = splits > 1 ? (float*)a.workspace : nullptr;
+  // GELU_D / MUL_AUX off the four-wave kernel: raw sums to a slab, the reduce runs the epilogue
+  const bool xs = ext_slab(a, splits);
+  if (xs) {
+    MMFD_CHECK_ARG(!a.a_rowsum, "mmfd_gemm: act %d with a_rowsum is not supported", act);
+    MMFD_CHECK_ARG(a.workspace && a.workspace_bytes >= (int64_t)splits * a.M * a.N * 4,
+                   "mmfd_gemm: act %d on this product needs a workspace of %lld bytes (mmfd_gemm_workspace_bytes)",
+                   act, (long long)((int64_t)splits * a.M * a.N * 4));
+  }
+  float* ws = (splits > 1 || xs) ? (float*)a.workspace : nullptr;
   const bool g8 = use_g8(a);
   // fused row sums: G8 writes them directly (one split) or as per-split partials after the slabs
   // row-sum partials after the split-K slabs: [splits][column tiles][M] when the workspace holds
@@ -730,7 +823,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   float* rs_out = rs_mode >= 2 ? rs_part : a.a_rowsum;
 
   if (xp.on) {
-    char* planes = (char*)a.workspace + align256((int64_t)(splits > 1 ? splits : 0) * a.M * a.N * 4 +
+    char* planes = (char*)a.workspace + align256((int64_t)(ws ? splits : 0) * a.M * a.N * 4 +
                                                  rowsum_ws_bytes(a, splits, true));
     const bf16* pa = (const bf16*)a.a_planes;
     const bf16* pb = (const bf16*)a.b_planes;

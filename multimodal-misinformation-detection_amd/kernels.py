@@ -395,6 +395,22 @@ def set_g4_persist(on=None):
     return bool(old)
 
 
+def g4_takes(x2d, W, act, residual=None, dropout_p=0.0):
+    """whether the four-wave GEMM runs x2d @ W^T (bf16 nn.Linear forward, contiguous operands) with
+    this epilogue — mirrors mmfd_gemmx::g4_epi's shape / mode conditions; blocks.linear saves the
+    GELU derivative (MMFD_ACT_GELU_D) only for products it takes (elsewhere GELU_D runs through a
+    split-K slab and the reduce, which costs more than the backward's erf it saves)"""
+    mode, kmax = g4_mode()
+    if mode == "off" or x2d.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
+        return False
+    if act in (ACT_GELU, ACT_GELU_D) and mode != "gelu":
+        return False
+    (M, Kd), N = x2d.shape, W.shape[0]
+    if M % 256 or N % 256 or Kd % 64 or Kd < 64 or Kd > kmax or residual is not None or dropout_p > 0:
+        return False
+    return _ld(x2d) % 8 == 0 and _ld(W) % 8 == 0 and x2d.data_ptr() % 16 == 0 and W.data_ptr() % 16 == 0
+
+
 def g4_mode():
     """(mode, kmax) the library currently uses for the four-wave GEMM"""
     return set_g4_mode()

@@ -342,16 +342,16 @@ int64_t g_g4_kmax = [] {
   const char* k = getenv("MMFD_G4_KMAX");
   return k ? (int64_t)atoll(k) : (int64_t)1024;
 }();
-bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_t s) {
+int g4_epi(const mmfd_gemm_args& a, const EpiArgs& e, int splits) {
   const int mode = g_g4_mode;
-  if (mode == 0) return false;
-  if (a.dtype != MMFD_BF16 || a.c_dtype != MMFD_BF16 || a.trans_a || a.trans_b || splits > 1) return false;
-  if (a.M % 256 || a.N % 256 || a.K % 64 || a.K < 64 || a.alpha != 1.0f || a.beta != 0.0f || a.a_rowsum) return false;
+  if (mode == 0) return -1;
+  if (a.dtype != MMFD_BF16 || a.c_dtype != MMFD_BF16 || a.trans_a || a.trans_b || splits > 1) return -1;
+  if (a.M % 256 || a.N % 256 || a.K % 64 || a.K < 64 || a.alpha != 1.0f || a.beta != 0.0f || a.a_rowsum) return -1;
   // K <= 1024: the short-K products (QKV, attention output, FFN1 at K = 768) gain from the register
   // epilogue; at K = 3072 (FFN2) the power-limited main loop is no faster than gemm256_kernel's and
   // ViT's FFN2 measured 10 % slower (profiles/r05_g4_vs_g8_vs_hipblaslt.log)
-  if (a.K > g_g4_kmax) return false;
-  if (!e.vec || e.pl || e.beta != 0.0f) return false;
+  if (a.K > g_g4_kmax) return -1;
+  if (!e.vec || e.pl || e.beta != 0.0f) return -1;
   // the epilogue modes of the encoder forward Linears (anything else runs on gemm256_kernel)
   int epi = -1;
   if (e.act == MMFD_ACT_NONE && !e.residual && e.p <= 0.0f) epi = 0;                    // QKV
@@ -366,14 +366,21 @@ bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_
   // K-contiguous (transposed) weight copy, blocks.linear_dx
   else if (e.act == MMFD_ACT_GELU_BWD && e.aux && !e.residual && e.p <= 0.0f) epi = 4;
   else if (e.act == MMFD_ACT_MUL_AUX && e.aux && !e.residual && e.p <= 0.0f) epi = 6;  // (its GELU_D form)
-  if (epi < 0) return false;
+  if (epi < 0) return -1;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (!al16(a.A) || !al16(a.B) || !al16(a.C)) return false;
-  if (a.lda % 8 || a.ldb % 8 || a.ldc % 8 || a.lda < a.K || a.ldb < a.K || a.ldc < a.N) return false;
+  if (!al16(a.A) || !al16(a.B) || !al16(a.C)) return -1;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 8 || a.lda < a.K || a.ldb < a.K || a.ldc < a.N) return -1;
   if (256 * a.lda * 2 >= (int64_t)1 << 31 || 256 * a.ldb * 2 >= (int64_t)1 << 31 || 256 * a.ldc * 2 >= (int64_t)1 << 31)
-    return false;
+    return -1;
   const int64_t tiles = (a.M / 256) * (a.N / 256);
-  if (tiles >= ((int64_t)1 << 31)) return false;
+  if (tiles >= ((int64_t)1 << 31)) return -1;
+  return epi;
+}
+
+bool launch_g4(const mmfd_gemm_args& a, const EpiArgs& e, int splits, hipStream_t s) {
+  const int epi = g4_epi(a, e, splits);
+  if (epi < 0) return false;
+  const int64_t tiles = (a.M / 256) * (a.N / 256);
   // persistent grid: one workgroup per CU (128 KB of LDS: one fits), each walking its tiles
   const int64_t grid = g_g4_persist ? std::min<int64_t>(tiles, g4_cus()) : tiles;
 #define G4_LAUNCH(E)                                                                                 \
