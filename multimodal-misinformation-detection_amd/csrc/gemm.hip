@@ -193,7 +193,11 @@ conv_mfma_kernel(const T* __restrict__ X, const T* __restrict__ B, int64_t ldb, 
 // and the reduce applies the whole epilogue. The tile kernels' shared epilogues (gemm_tiles.h) keep
 // their round-5 code — the two extra activations inlined there made every GEMM's epilogue slower
 // (config-5 extract −4 %, profiles/r06t_extract_regression.log).
-__device__ __forceinline__ bool act_ext(int act) { return act == MMFD_ACT_GELU_D || act == MMFD_ACT_MUL_AUX; }
+// The forward-only tanh / sigmoid (the cross-encoder's pooler and score) go the same way: the tile
+// kernels' epilogues carry only NONE / GELU / ReLU and their backward forms.
+__device__ __host__ __forceinline__ bool act_ext(int act) {
+  return act == MMFD_ACT_GELU_D || act == MMFD_ACT_MUL_AUX || act == MMFD_ACT_TANH || act == MMFD_ACT_SIGMOID;
+}
 
 // epilogue_store (gemm_tiles.h) with the two extra activations: bias, [residual first], the
 // activation, then the unchanged tail (dropout, residual, beta, store / planes)
@@ -208,8 +212,10 @@ __device__ __forceinline__ void epilogue_store_x(const EpiArgs& e, TC* C, int64_
     float d;
     z = gelu_and_grad_f(z, d);
     if (e.aux) *ax = from_f32<TC>(d);
-  } else {
+  } else if (e.act == MMFD_ACT_MUL_AUX) {
     z *= to_f32(*ax);
+  } else {
+    z = act_tail_f(e.act, z);
   }
   EpiArgs t = e;
   t.act = MMFD_ACT_NONE; t.bias = nullptr;
@@ -237,11 +243,14 @@ __device__ __forceinline__ void epilogue_store8_x(const EpiArgs& e, TC* C, int64
 #pragma unroll
     for (int q = 0; q < 8; ++q) z[q] = gelu_and_grad_f(z[q], d[q]);
     if (e.aux) V8<TC>::store(ax, d);
-  } else {
+  } else if (e.act == MMFD_ACT_MUL_AUX) {
     float a[8];
     V8<TC>::load(ax, a);
 #pragma unroll
     for (int q = 0; q < 8; ++q) z[q] *= a[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] = act_tail_f(e.act, z[q]);
   }
   EpiArgs t = e;
   t.act = MMFD_ACT_NONE; t.bias = nullptr;
@@ -676,7 +685,7 @@ EpiArgs make_epi(const mmfd_gemm_args& a) {
 // kernels write raw sums to a slab (at least one split) and the reduce runs the epilogue
 bool ext_slab(const mmfd_gemm_args& a, int splits) {
   const int act = a.ep.act;
-  if (act != MMFD_ACT_GELU_D && act != MMFD_ACT_MUL_AUX) return false;
+  if (!act_ext(act)) return false;
   if (splits == 1 && use_g8(a) && a.dtype == MMFD_BF16 && a.c_dtype == MMFD_BF16 && !a.conv &&
       mmfd_gemmx::g4_epi(a, make_epi(a), splits) >= 0)
     return false;
