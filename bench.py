@@ -209,7 +209,7 @@ def extract_leg(args, dev, world, rank, precision):
     prof = probe.summary()
     dom_name, d = max(((k, v) for k, v in prof.items() if "split-K" not in k), key=lambda kv: kv[1]["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-    x6 = "x6f_kernel" in dom_name or dom_name.rstrip().endswith("true>")
+    x6 = "_x6f" in dom_name or dom_name.rstrip().endswith("true>")
     peak = PEAK_TFLOPS[precision] if not x6 else PEAK_TFLOPS["bf16"] / 6
     traffic, traffic_src = pmc_traffic(dom_name)
     ips = args.batch * args.steps / (t_img * 1e-3)
@@ -976,7 +976,7 @@ def train_leg(args, dev, world, rank, precision):
     # GEMM (gemm_x6f.hip; gemm.hip X6) runs each fp32 product as six bf16 MFMA products, so its
     # ceiling is the bf16 dense MFMA peak / 6 (= 419.4 TFLOP/s of fp32 products), not the fp32 MFMA peak
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-    x6 = "x6f_kernel" in dom_name or dom_name.rstrip().endswith("true>")
+    x6 = "_x6f" in dom_name or dom_name.rstrip().endswith("true>")
     peak = PEAK_TFLOPS[precision] if not x6 else PEAK_TFLOPS["bf16"] / 6
     gemm_ms = sum(v["ms"] for v in prof.values()) / steps_in_prof
     gemm_tf = sum(v["flops"] for v in prof.values()) / (sum(v["ms"] for v in prof.values()) * 1e-3) / 1e12
