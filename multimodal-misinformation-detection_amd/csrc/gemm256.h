@@ -17,12 +17,15 @@ namespace {
 // PRE: the epilogue has exactly one bf16 operand stream (residual, saved pre-activation or C),
 // prefetched for all of a thread's rows before the accumulators are staged (see the epilogue)
 
-template <typename T, int TA, int TB, typename TC, bool PRE, bool X6>
-__global__ void __launch_bounds__(NT, 1)
-gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
-               TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
-               float alpha, int tiles_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
-               int rs_mode, int group_m, X6Args x6) {
+// LEAN: no activation and no dropout in the epilogue (or split-K slabs): the epilogue's fast path
+// compiles without that code (g8_epilogue); gemm256_kernel is the lean instantiation, gemm256_act_kernel
+// the full one (as gemm256_x6f_kernel / gemm256_x6f_act_kernel)
+template <typename T, int TA, int TB, typename TC, bool PRE, bool X6, bool LEAN>
+__device__ __forceinline__ void
+gemm256_body(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+             TC* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
+             float alpha, int tiles_per_split, const EpiArgs& e, float* __restrict__ rs_out, float rs_beta,
+             int rs_mode, int group_m, const X6Args& x6) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -331,8 +334,21 @@ gemm256_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     }
   }
 
-  g8_epilogue<TC, PRE>(acc, smem, e, C, ldc, ws, split, M, N, alpha, m0, n0, tid, lane, wave, wr, wc);
+  g8_epilogue<TC, PRE, LEAN>(acc, smem, e, C, ldc, ws, split, M, N, alpha, m0, n0, tid, lane, wave, wr, wc);
 }
+
+#define G8_KERNEL(NAME, LEAN)                                                                           \
+  template <typename T, int TA, int TB, typename TC, bool PRE, bool X6>                               \
+  __global__ void __launch_bounds__(NT, 1)                                                            \
+  NAME(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, TC* __restrict__ C, \
+       int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K, float alpha, int tiles_per_split, \
+       EpiArgs e, float* __restrict__ rs_out, float rs_beta, int rs_mode, int group_m, X6Args x6) {      \
+    gemm256_body<T, TA, TB, TC, PRE, X6, LEAN>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, tiles_per_split, e, \
+                                              rs_out, rs_beta, rs_mode, group_m, x6);                  \
+  }
+G8_KERNEL(gemm256_kernel, true)
+G8_KERNEL(gemm256_act_kernel, false)
+#undef G8_KERNEL
 
 int g8_group_m() {
   static const int gm = getenv("MMFD_G8_GROUP_M") ? std::max(1, atoi(getenv("MMFD_G8_GROUP_M"))) : 1;
@@ -345,12 +361,19 @@ void launch_g8_v(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int split
   dim3 grid((unsigned)((a.N + G8_BN - 1) / G8_BN), (unsigned)((a.M + G8_BM - 1) / G8_BM), (unsigned)splits);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<T, TA, TB, TC, PRE, X6>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess &&
+           hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_act_kernel<T, TA, TB, TC, PRE, X6>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE, X6>), grid, dim3(NT), G8_LDS, s, (const T*)A, lda,
-                     (const T*)B, ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
-                     a.a_rowsum_beta, rs_mode, g8_group_m(), x6);
+  if (ws != nullptr || (e.act == MMFD_ACT_NONE && e.p <= 0.f))
+    hipLaunchKernelGGL((gemm256_kernel<T, TA, TB, TC, PRE, X6>), grid, dim3(NT), G8_LDS, s, (const T*)A, lda,
+                       (const T*)B, ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
+                       a.a_rowsum_beta, rs_mode, g8_group_m(), x6);
+  else
+    hipLaunchKernelGGL((gemm256_act_kernel<T, TA, TB, TC, PRE, X6>), grid, dim3(NT), G8_LDS, s, (const T*)A, lda,
+                       (const T*)B, ldb, (TC*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, tps, e, rs_out,
+                       a.a_rowsum_beta, rs_mode, g8_group_m(), x6);
 }
 
 }  // namespace

@@ -434,12 +434,13 @@ def _kernel_name(a, split):
         streams = int(bool(a.ep.residual)) + int(a.ep.act in (ACT_GELU_BWD, ACT_RELU_BWD, ACT_MUL_AUX)) + int(a.beta != 0.0)
         pre = a.c_dtype == BF16 and streams == 1 and not split
         x6 = _x6(a)
-        if x6 == 2:  # gemm_x6f.hip launch_x6f: the lean instantiation without an activation / dropout
-            lean = split or (a.ep.act == ACT_NONE and a.ep.dropout_p <= 0.0)
+        # the lean instantiations (no activation / dropout, or split-K slabs) keep the plain names
+        lean = split or (a.ep.act == ACT_NONE and a.ep.dropout_p <= 0.0)
+        if x6 == 2:  # gemm_x6f.hip launch_x6f
             base = f"gemm256_x6f{'' if lean else '_act'}_kernel<{a.trans_a}, {a.trans_b}>"
-        else:
-            base = (f"gemm256_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, {t[a.c_dtype]}, "
-                    f"{'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
+        else:  # gemm256.h launch_g8_v
+            base = (f"gemm256{'' if lean else '_act'}_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, "
+                    f"{t[a.c_dtype]}, {'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
     elif a.N <= 64 and not a.trans_b:  # gemm.hip launch_mfma: the 256x64 tile
         base = f"gemm_mfma_n64_kernel<{t[a.dtype]}, {a.trans_a}, {t[a.c_dtype]}>"
     else:
