@@ -1113,3 +1113,38 @@ def test_embed_bwd_deterministic_scatter_add(dtype, B, L, D, V):
     torch.cuda.synchronize()
     rw = base[0].double().cpu().index_add(0, i, x)
     assert (dword.double().cpu() - rw).abs().max().item() <= 1e-5 * max(1.0, rw.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_ext_acts_full_epilogue_through_reduce(dtype):
+    """MMFD_ACT_MUL_AUX / MMFD_ACT_GELU_D off the four-wave kernel run through a split-K slab and the
+    reduce's epilogue (gemm.hip epilogue_store8_x): with dropout, a residual and beta the result equals
+    the tile kernels' GELU_BWD / GELU path on the same inputs — bit for bit in fp32 (the saved
+    derivative is gelu_grad_f of the same fp32 pre-activation), within bf16 rounding in bf16"""
+    M, N, Kd = 512, 384, 256  # N not a multiple of 256: never the four-wave kernel
+    x = _rand(M, Kd, dtype=dtype, seed=91).to(DEV)
+    w = _rand(N, Kd, dtype=dtype, seed=92, scale=0.1).to(DEV)
+    b = _rand(N, seed=93).to(DEV)
+    res = _rand(M, N, dtype=dtype, seed=94).to(DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=dtype)
+    d = torch.empty(M, N, device=DEV, dtype=dtype)
+    seed = K.Seed(95, device=DEV)
+    kw = dict(bias=b, residual=res, dropout_p=0.1, seed=seed, salt=9)
+    y_g = K.gemm(x, w, act=K.ACT_GELU, aux=pre, **kw)
+    y_d = K.gemm(x, w, act=K.ACT_GELU_D, aux=d, **kw)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert torch.equal(y_g, y_d), (y_g - y_d).abs().max().item()
+    else:
+        assert (y_g.float() - y_d.float()).abs().max().item() <= y_g.float().abs().max().item() * 2.0 ** -7
+    dy = _rand(M, Kd, dtype=dtype, seed=96).to(DEV)
+    w2 = _rand(Kd, N, dtype=dtype, seed=97, scale=0.1).to(DEV)
+    c0 = _rand(M, N, dtype=dtype, seed=98).to(DEV)
+    c1, c2 = c0.clone(), c0.clone()
+    K.gemm(dy, w2, trans_b=True, act=K.ACT_GELU_BWD, aux=pre, out=c1, beta=1.0, **kw)
+    K.gemm(dy, w2, trans_b=True, act=K.ACT_MUL_AUX, aux=d, out=c2, beta=1.0, **kw)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert torch.equal(c1, c2), (c1 - c2).abs().max().item()
+    else:
+        assert (c1.float() - c2.float()).abs().max().item() <= c1.float().abs().max().item() * 2.0 ** -6
