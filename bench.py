@@ -138,11 +138,19 @@ def cpu_baseline(dev, steps=3, batch=4):
     return out, parity
 
 
+# the PMC summaries taken on the current tree (tools/gpu_final.sh): looked up first, then the other
+# committed summaries newest tag first (a kernel renamed since is then found under an older tag)
+PMC_TAGS = ("r06zzz_fp32", "r06zzz_bf16")
+
+
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary that lists it
-    (tools/profile.sh -> profiles/<tag>_hbm_traffic.json: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    """HBM bytes per launch of `kernel` from the committed PMC summaries (tools/profile.sh ->
+    profiles/<tag>_hbm_traffic.json: FETCH_SIZE x2 + WRITE_SIZE): the current tree's (PMC_TAGS), else
+    the newest that lists it, or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")))
+    first = [os.path.join(ROOT, "profiles", f"{t}_hbm_traffic.json") for t in PMC_TAGS]
+    files = [f for f in files if f not in first] + [f for f in reversed(first) if os.path.exists(f)]
     for path in reversed(files):
         with open(path) as f:
             k = json.load(f).get("kernels", {}).get(kernel)
