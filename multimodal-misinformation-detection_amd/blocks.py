@@ -374,9 +374,9 @@ def as2d(x):
 # linear
 # -------------------------------------------------------------------------------------------------
 # the training forward's GELU keeps gelu'(pre-activation) instead of the pre-activation
-# (MMFD_ACT_GELU_D; one erf per element instead of one in the forward and one in the backward) when
-# the four-wave GEMM runs the product (bf16: its register epilogue computes both); MMFD_GELU_DERIV=0
-# keeps the pre-activation (A/B switch)
+# (MMFD_ACT_GELU_D; one erf per element instead of one in the forward and one in the backward) when a
+# kernel with it in its own epilogue runs the product (bf16: the four-wave GEMM; fp32: the
+# split-operand GEMM's ext instantiation); MMFD_GELU_DERIV=0 keeps the pre-activation (A/B switch)
 GELU_DERIV = os.environ.get("MMFD_GELU_DERIV", "1") != "0"
 
 
@@ -388,7 +388,10 @@ def linear(ctx: StepCtx, x2d, name, *, act=K.ACT_NONE, keep_aux=False, residual=
     aux = None
     if keep_aux and act in (K.ACT_GELU, K.ACT_RELU):
         aux = torch.empty((x2d.shape[0], W.shape[0]), device=x2d.device, dtype=out_dtype or ctx.dt)
-        if act == K.ACT_GELU and GELU_DERIV and residual is None and drop_site is None and K.g4_takes(x2d, W, act):
+        # (bf16: the four-wave kernel's register epilogue; fp32: the split-operand kernel's ext
+        # instantiation — planes of x given means the product runs on split operands)
+        if act == K.ACT_GELU and GELU_DERIV and residual is None and drop_site is None and (
+                K.g4_takes(x2d, W, act) or (ctx.dt == torch.float32 and xp is not None)):
             act = K.ACT_GELU_D
             aux._mmfd_gelu_d = True
     y = K.gemm(x2d, W, bias=ctx.b(name), act=act, aux=aux, residual=residual, out_dtype=out_dtype or ctx.dt,

@@ -683,11 +683,17 @@ EpiArgs make_epi(const mmfd_gemm_args& a) {
 
 // a GELU_D / MUL_AUX product on the MFMA paths that the four-wave kernel does not take: the tile
 // kernels write raw sums to a slab (at least one split) and the reduce runs the epilogue
-bool ext_slab(const mmfd_gemm_args& a, int splits) {
+bool ext_slab(const mmfd_gemm_args& a, int splits, bool x6_on) {
   const int act = a.ep.act;
   if (!act_ext(act)) return false;
   if (splits == 1 && use_g8(a) && a.dtype == MMFD_BF16 && a.c_dtype == MMFD_BF16 && !a.conv &&
       mmfd_gemmx::g4_epi(a, make_epi(a), splits) >= 0)
+    return false;
+  // the split-operand kernel's ext instantiation: GELU_D / MUL_AUX without dropout, one split, and
+  // every tile on the epilogue's fast path (full 256x256 tiles, 16-B aligned operands: its per-element
+  // path for partial tiles is the shared one, which does not carry the two)
+  if (splits == 1 && (act == MMFD_ACT_GELU_D || act == MMFD_ACT_MUL_AUX) && a.ep.dropout_p <= 0.f && !a.conv &&
+      x6_on && x6_fused() && a.M % 256 == 0 && a.N % 256 == 0 && make_epi(a).vec)
     return false;
   return true;
 }
@@ -707,7 +713,7 @@ extern "C" int64_t mmfd_gemm_workspace_bytes(const mmfd_gemm_args* a) {
   const X6Plan xp = x6_plan(*a);
   int64_t need = 0;
   const int splits = choose_splits(*a, &need, xp.on);
-  if (ext_slab(*a, splits) && need < a->M * a->N * 4) need = a->M * a->N * 4;
+  if (ext_slab(*a, splits, xp.on) && need < a->M * a->N * 4) need = a->M * a->N * 4;
   need += rowsum_ws_bytes(*a, splits, use_g8(*a));
   if (xp.on)  // + the bf16 planes of the operands not handed over already split
     need = align256(need) + (a->a_planes ? 0 : align256(3 * xp.pa)) + (a->b_planes ? 0 : 3 * xp.pb);
@@ -809,7 +815,7 @@ extern "C" int mmfd_gemm(const mmfd_gemm_args* ap, mmfd_stream_t stream) {
   splits = tps > 0 ? (nkt + tps - 1) / tps : 1;
   if (splits < 1) splits = 1;
   // GELU_D / MUL_AUX off the four-wave kernel: raw sums to a slab, the reduce runs the epilogue
-  const bool xs = ext_slab(a, splits);
+  const bool xs = ext_slab(a, splits, xp.on);  // (xp.on as decided above: the workspace held the planes)
   if (xs) {
     MMFD_CHECK_ARG(!a.a_rowsum, "mmfd_gemm: act %d with a_rowsum is not supported", act);
     MMFD_CHECK_ARG(a.workspace && a.workspace_bytes >= (int64_t)splits * a.M * a.N * 4,

@@ -223,7 +223,7 @@ __device__ __forceinline__ float xf_sum3(uint4 h, uint4 m, uint4 l) {
 // CONV: implicit-GEMM convolution (ConvGeom): A is the planes [3][N*H*W][C] of the NHWC activation,
 // its fill gathers the im2col rows per K-step (XfConvFill); TA = 0 only. The body is shared by
 // gemm256_x6f_kernel and conv_x6f_kernel (the plain GEMM keeps its kernel name in traces)
-template <int TA, int TB, bool CONV, bool LEAN = false>
+template <int TA, int TB, bool CONV, bool LEAN = false, bool EXT = false>
 __device__ __forceinline__ void
 x6f_body(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
          float* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
@@ -445,7 +445,7 @@ x6f_body(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, in
       if (r1 < M) dst[r1] = (bt != 0.f ? bt * dst[r1] : 0.f) + rs1;
     }
   }
-  g8_epilogue<float, false, LEAN>(acc, smem, e, C, ldc, ws, split, M, N, alpha, m0, n0, tid, lane, wave, wr, wc);
+  g8_epilogue<float, false, LEAN, EXT>(acc, smem, e, C, ldc, ws, split, M, N, alpha, m0, n0, tid, lane, wave, wr, wc);
 #ifdef MMFD_XF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   XF_TSTAMP(18);
@@ -474,6 +474,17 @@ gemm256_x6f_act_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __re
   x6f_body<TA, TB, false, false>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, steps_per_split, e, rs_out, rs_beta,
                                  rs_mode, x6, ConvGeom{});
 }
+// MMFD_ACT_GELU_D / MMFD_ACT_MUL_AUX without dropout (the fp32 training FFN's GELU with its derivative
+// saved, and the data gradient through it)
+template <int TA, int TB>
+__global__ void __launch_bounds__(NT, 1)
+gemm256_x6f_ext_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+                       float* __restrict__ C, int64_t ldc, float* __restrict__ ws, int64_t M, int64_t N, int64_t K,
+                       float alpha, int steps_per_split, EpiArgs e, float* __restrict__ rs_out, float rs_beta,
+                       int rs_mode, X6Args x6) {
+  x6f_body<TA, TB, false, false, true>(A, lda, B, ldb, C, ldc, ws, M, N, K, alpha, steps_per_split, e, rs_out, rs_beta,
+                                       rs_mode, x6, ConvGeom{});
+}
 // implicit-GEMM convolution on split operands (mmfd_gemm_args.conv): X = the activation's planes
 __global__ void __launch_bounds__(NT, 1)
 conv_x6f_kernel(const bf16* __restrict__ X, const bf16* __restrict__ B, int64_t ldb, float* __restrict__ C,
@@ -501,6 +512,8 @@ void launch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_x6f_kernel<TA, TB>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess &&
            hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_x6f_act_kernel<TA, TB>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess &&
+           hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_x6f_ext_kernel<TA, TB>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS) == hipSuccess;
   }();
   (void)attr;
@@ -508,7 +521,12 @@ void launch_x6f(const mmfd_gemm_args& a, const EpiArgs& e, float* ws, int splits
   const int64_t lda = TA == 0 ? a.K : a.M, ldb = TB == 0 ? a.K : a.N;
   // (with split-K slabs the tile kernel runs no epilogue at all: the reduce does)
   const bool lean = ws != nullptr || (e.act == MMFD_ACT_NONE && e.p <= 0.f);
-  if (lean)
+  const bool ext = !lean && (e.act == MMFD_ACT_GELU_D || e.act == MMFD_ACT_MUL_AUX);  // (no dropout: gemm.hip ext_slab)
+  if (ext)
+    hipLaunchKernelGGL((gemm256_x6f_ext_kernel<TA, TB>), grid, dim3(NT), G8_LDS, s, (const bf16*)pa, lda,
+                       (const bf16*)pb, ldb, (float*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, sps, e, rs_out,
+                       a.a_rowsum_beta, rs_mode, x6);
+  else if (lean)
     hipLaunchKernelGGL((gemm256_x6f_kernel<TA, TB>), grid, dim3(NT), G8_LDS, s, (const bf16*)pa, lda, (const bf16*)pb,
                        ldb, (float*)a.C, a.ldc, ws, a.M, a.N, a.K, a.alpha, sps, e, rs_out, a.a_rowsum_beta, rs_mode, x6);
   else

@@ -436,8 +436,9 @@ def _kernel_name(a, split):
         x6 = _x6(a)
         # the lean instantiations (no activation / dropout, or split-K slabs) keep the plain names
         lean = split or (a.ep.act == ACT_NONE and a.ep.dropout_p <= 0.0)
-        if x6 == 2:  # gemm_x6f.hip launch_x6f
-            base = f"gemm256_x6f{'' if lean else '_act'}_kernel<{a.trans_a}, {a.trans_b}>"
+        if x6 == 2:  # gemm_x6f.hip launch_x6f (ext: GELU_D / MUL_AUX in the kernel's own epilogue)
+            ext = not lean and a.ep.act in (ACT_GELU_D, ACT_MUL_AUX)
+            base = f"gemm256_x6f{'' if lean else '_ext' if ext else '_act'}_kernel<{a.trans_a}, {a.trans_b}>"
         else:  # gemm256.h launch_g8_v
             base = (f"gemm256{'' if lean else '_act'}_kernel<{t[BF16 if x6 else a.dtype]}, {a.trans_a}, {a.trans_b}, "
                     f"{t[a.c_dtype]}, {'true' if pre else 'false'}, {'true' if x6 else 'false'}>")
