@@ -140,7 +140,7 @@ def cpu_baseline(dev, steps=3, batch=4):
 
 # the PMC summaries taken on the current tree (tools/gpu_final.sh): looked up first, then the other
 # committed summaries newest tag first (a kernel renamed since is then found under an older tag)
-PMC_TAGS = ("r06zzz_fp32", "r06zzz_bf16")
+PMC_TAGS = ("r06zzzz_fp32", "r06zzzz_bf16")
 
 
 def pmc_traffic(kernel):
